@@ -1,0 +1,179 @@
+/* pbftv.h -- C ABI of the MI355X batch verifier for simple_pbft's crypto hot path.
+ *
+ * Drop-in boundary.  The reference (1556174776/simple_pbft,
+ * Go) has no FFI; the functions below are what a thin cgo shim binds so the
+ * Go call sites keep their signatures (INTEGRATION.md shows the binding):
+ *
+ *   pbftv_hash_hex            <- utils.Hash(content []byte) string          utils/utils.go:13-17
+ *   pbftv_sha256_batch        <- batched utils.Hash over a pool snapshot   utils/utils.go:13-17
+ *   pbftv_gojson_*            <- json.Marshal preimages hashed by digest() pbft/consensus/pbft_impl.go:235-243,
+ *                                                                          pbft/consensus/pbft_msg_types.go:3-38
+ *   pbftv_digest_request_batch<- digest(*RequestMsg) for many requests     pbft/consensus/pbft_impl.go:73,235-243
+ *   pbftv_digest_check_batch  <- digest recompute + compare per message    pbft/consensus/pbft_impl.go:190-199
+ *   pbftv_verify_msg_batch    <- State.verifyMsg over a vote snapshot      pbft/consensus/pbft_impl.go:176-202
+ *   pbftv_register_keys       <- per-node public-key table (planned by the author next to
+ *                                NodeTable, 需要改进的地方.md:17 / pbft/network/node.go:60-65)
+ *   pbftv_ecdsa_p256_verify_batch <- Go crypto/ecdsa.Verify per signed pool message
+ *                                (absent in the reference)
+ *   pbftv_qc_verify           <- quorum count of prepared()/committed()    pbft/consensus/pbft_impl.go:207-232
+ *
+ * Conventions
+ *   - The caller owns every buffer; the library never keeps a pointer after a
+ *     call returns (cgo rule: no Go pointers retained by C).
+ *   - Host-buffer calls are synchronous.  *_dev calls take device pointers on
+ *     one of the context's devices and enqueue on `stream` (a hipStream_t, or
+ *     NULL for the context's stream of that device) without synchronising.
+ *   - Return 0 on success, negative PBFTV_E* on API / device errors.  A failed
+ *     signature or digest is never an error: it is a 0 bit.
+ *   - Bitmaps are LSB-first: bit i of the batch is (bitmap[i/8] >> (i%8)) & 1.
+ *   - Big-endian 32-byte integers (hash, r, s, X, Y) exactly as Go's
+ *     big.Int.FillBytes / elliptic.Marshal would lay them out.
+ *   - A context is safe to share across threads (one lock per device).
+ *   - There is no CPU fallback: with no usable gfx950 device pbftv_open fails
+ *     with PBFTV_ENODEV.
+ */
+#ifndef PBFTV_H
+#define PBFTV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBFTV_OK 0
+#define PBFTV_EINVAL (-1)   /* bad argument (null pointer, bad device index, ...) */
+#define PBFTV_ENODEV (-2)   /* no usable GPU in device_mask */
+#define PBFTV_EDEVICE (-3)  /* HIP runtime / kernel error; see pbftv_last_error() */
+#define PBFTV_ENOMEM (-4)   /* device or pinned host allocation failed */
+#define PBFTV_ENOKEYS (-5)  /* verify called before pbftv_register_keys */
+
+typedef struct pbftv_ctx pbftv_ctx;
+
+/* Open a context on the GPUs in device_mask (bit d = HIP device d; 0 = all
+ * visible).  Batches passed to the host-buffer calls are split into
+ * contiguous shards, one per device (no collective: the shards are
+ * independent and the bitmaps are concatenated). */
+int pbftv_open(pbftv_ctx** out, uint32_t device_mask);
+void pbftv_close(pbftv_ctx* ctx);
+int pbftv_device_count(const pbftv_ctx* ctx);
+/* HIP device id of the context's i-th device, or -1. */
+int pbftv_device_id(const pbftv_ctx* ctx, int i);
+const char* pbftv_strerror(int code);
+/* Last error message of the calling thread ("" if none). */
+const char* pbftv_last_error(void);
+/* Pre-size per-device scratch for batches of up to n items (optional). */
+int pbftv_reserve(pbftv_ctx* ctx, uint64_t n);
+
+/* ---- device memory / stream plumbing ---------------------------------- */
+/* For callers that keep pool snapshots resident in HBM (and for bench.py):
+ * plain allocations on the context's device index dev, copies on that
+ * device's stream (synchronous), and a stream synchronise. */
+int pbftv_dev_alloc(pbftv_ctx* ctx, int dev, uint64_t bytes, void** out_ptr);
+int pbftv_dev_free(pbftv_ctx* ctx, int dev, void* ptr);
+int pbftv_memcpy_h2d(pbftv_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes);
+int pbftv_memcpy_d2h(pbftv_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes);
+int pbftv_memset_dev(pbftv_ctx* ctx, int dev, void* dst, int value, uint64_t bytes);
+/* The context's stream of device dev as a hipStream_t (for *_dev calls). */
+void* pbftv_stream(pbftv_ctx* ctx, int dev);
+int pbftv_stream_sync(pbftv_ctx* ctx, int dev);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around every
+ * kernel launch while enabled.  kernel: 0 = ecdsa scalars, 1 = ecdsa comb,
+ * 2 = sha256.  pbftv_kernel_time_ms synchronises the device's stream and
+ * returns the summed milliseconds and the launch count since the last reset. */
+#define PBFTV_K_ECDSA_SCALARS 0
+#define PBFTV_K_ECDSA_COMB 1
+#define PBFTV_K_SHA256 2
+int pbftv_set_kernel_timing(pbftv_ctx* ctx, int enable);
+int pbftv_kernel_time_ms(pbftv_ctx* ctx, int dev, int kernel, double* out_ms, uint64_t* out_launches);
+int pbftv_reset_kernel_times(pbftv_ctx* ctx);
+
+/* ---- SHA-256 digests (utils.Hash) ------------------------------------ */
+
+/* utils.Hash(content): lowercase hex SHA-256, 64 chars + NUL into out_hex. */
+int pbftv_hash_hex(pbftv_ctx* ctx, const uint8_t* content, uint64_t len, char out_hex[65]);
+
+/* n messages at data+offsets[i], lengths[i] bytes -> out_digests (n*32 raw bytes). */
+int pbftv_sha256_batch(pbftv_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                       uint64_t n, uint8_t* out_digests);
+
+/* As above, plus compare against expected (n*32): bit i = digest matches. */
+int pbftv_digest_check_batch(pbftv_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                             const uint8_t* expected, uint64_t n, uint8_t* out_bitmap);
+
+/* Device-resident form on device index dev (0..pbftv_device_count-1).  The
+ * data buffer must be readable 4 bytes past the end of every message
+ * (pbftv_dev_alloc / hipMalloc allocations are).  order (may be NULL) is a lane ->
+ * message permutation; pbftv_sha256_order_dev builds one that groups messages
+ * by block count.  d_expected/d_bitmap may be NULL (digests only); d_bitmap
+ * must be ceil(n/32)*4 bytes when used. */
+int pbftv_sha256_batch_dev(pbftv_ctx* ctx, int dev, const uint8_t* d_data, const uint64_t* d_offsets,
+                           const uint32_t* d_lengths, const uint32_t* d_order, uint64_t n, uint8_t* d_digests,
+                           const uint8_t* d_expected, uint8_t* d_bitmap, void* stream);
+int pbftv_sha256_order_dev(pbftv_ctx* ctx, int dev, const uint32_t* d_lengths, uint64_t n, uint32_t* d_order,
+                           void* stream);
+
+/* ---- Go-JSON digest preimages (json.Marshal of pbft_msg_types.go) ----- */
+/* Each writes at most cap bytes to out and returns the full encoded length
+ * (call with cap = 0 to size).  Strings are byte strings (ptr, len) and may
+ * hold arbitrary bytes; encoding follows Go 1.19 encoding/json exactly. */
+uint64_t pbftv_gojson_request(int64_t timestamp, const char* client_id, uint64_t client_id_len, const char* operation,
+                              uint64_t operation_len, int64_t sequence_id, uint8_t* out, uint64_t cap);
+uint64_t pbftv_gojson_vote(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                           const char* node_id, uint64_t node_id_len, int64_t msg_type, uint8_t* out, uint64_t cap);
+uint64_t pbftv_gojson_reply(int64_t view_id, int64_t timestamp, const char* client_id, uint64_t client_id_len,
+                            const char* node_id, uint64_t node_id_len, const char* result, uint64_t result_len,
+                            uint8_t* out, uint64_t cap);
+uint64_t pbftv_gojson_preprepare(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                                 int has_request, int64_t req_timestamp, const char* req_client_id,
+                                 uint64_t req_client_id_len, const char* req_operation, uint64_t req_operation_len,
+                                 int64_t req_sequence_id, uint8_t* out, uint64_t cap);
+
+/* digest(*RequestMsg) for n requests: Go-JSON preimages built on the host,
+ * hashed in one GPU batch.  client_ids/operations are concatenated byte
+ * strings with per-item offsets/lengths.  out_digests: n*32 raw bytes. */
+int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
+                               const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
+                               const uint64_t* operation_off, const uint32_t* operation_len,
+                               const int64_t* sequence_ids, uint8_t* out_digests);
+
+/* State.verifyMsg (pbft_impl.go:176-202) over n votes against one state:
+ * bit i = view_ids[i] == state_view_id
+ *         && (state_last_seq == -1 || state_last_seq < sequence_ids[i])
+ *         && digest_got[i] (digest_got_len[i] bytes at digest_got + digest_got_off[i])
+ *            is exactly the lowercase hex of req_digest (Go string compare). */
+int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const uint8_t req_digest[32], uint64_t n,
+                           const int64_t* view_ids, const int64_t* sequence_ids, const char* digest_got,
+                           const uint64_t* digest_got_off, const uint32_t* digest_got_len, uint8_t* out_bitmap);
+
+/* ---- ECDSA-P256 signatures (Go crypto/ecdsa.Verify semantics) --------- */
+
+/* Register the replica public keys (k * 64 B, X||Y big-endian); replaces any
+ * previous table.  out_valid[j] = 1 if key j is a valid P-256 point (0 <= X,Y
+ * < p and on the curve); signatures naming an invalid key always fail.  Builds
+ * the per-key fixed-base comb tables (about 264 KiB per key) on every device. */
+int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid);
+
+/* Verify n signatures: hashes (n*32), sig_rs (n*64: r||s big-endian),
+ * key_idx (n, index into the registered table).  out_bitmap: ceil(n/8) B. */
+int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs,
+                                  const uint32_t* key_idx, uint64_t n, uint8_t* out_bitmap);
+
+/* Device-resident form (device index dev); hashes/sigs 16-B aligned;
+ * d_bitmap: ceil(n/8) B.  Enqueued on stream, not synchronised. */
+int pbftv_ecdsa_p256_verify_batch_dev(pbftv_ctx* ctx, int dev, const uint8_t* d_hashes, const uint8_t* d_sig_rs,
+                                      const uint32_t* d_key_idx, uint64_t n, uint8_t* d_bitmap, void* stream);
+
+/* Quorum certificate: verify n signatures and count acceptances.
+ * *out_accepted = popcount; *out_quorum = (*out_accepted >= quorum).  With
+ * quorum = 2f this is the reference's prepared()/committed() count
+ * (pbft_impl.go:212,227); with 2f+1 it is a PBFT certificate. */
+int pbftv_qc_verify(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs, const uint32_t* key_idx, uint64_t n,
+                    uint32_t quorum, uint8_t* out_bitmap, uint64_t* out_accepted, int* out_quorum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBFTV_H */

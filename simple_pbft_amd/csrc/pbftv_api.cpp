@@ -1,0 +1,648 @@
+// pbftv_api.cpp -- the C ABI of include/pbftv.h on top of the gfx950 kernels.
+//
+// One pbftv_ctx owns, per GPU: a non-blocking HIP stream, the comb tables of
+// G and every registered key (resident in HBM: ~264 KiB per key), and
+// grow-only scratch.  Host-buffer batches are cut into contiguous shards
+// (multiples of 512 items, so every shard's bitmap starts on a byte and every
+// wave on a 64-item boundary), one per device, each driven by its own host
+// thread; the shards are independent and the bitmaps are concatenated -- no
+// collective.  There is no CPU path: if no gfx950 device is
+// usable, pbftv_open fails with PBFTV_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/pbftv.h"
+#include "gojson.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                                         \
+  do {                                                                                                        \
+    hipError_t e_ = (expr);                                                                                   \
+    if (e_ != hipSuccess)                                                                                     \
+      return fail(e_ == hipErrorOutOfMemory ? PBFTV_ENOMEM : PBFTV_EDEVICE,                                   \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                                         \
+  } while (0)
+
+// grow-only device buffer
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+struct Device {
+  int id = -1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  // signature state
+  DevBuf tables, key_valid;
+  uint32_t nkeys = 0;
+  bool have_keys = false;
+  // ecdsa scratch
+  DevBuf hashes, sigs, key_idx, scal, flag, bitmap;
+  // sha scratch
+  DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
+  // kernel timing (events recorded around launches while ctx timing is on)
+  const bool* timing = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[3];
+  double acc_ms[3] = {0, 0, 0};
+  uint64_t launches[3] = {0, 0, 0};
+};
+
+// record start/stop events around one launch when timing is enabled
+template <class F>
+hipError_t timed(Device& d, int k, hipStream_t st, F launch) {
+  if (!d.timing || !*d.timing) return launch();
+  hipEvent_t a, b;
+  hipError_t e = hipEventCreate(&a);
+  if (e != hipSuccess) return e;
+  e = hipEventCreate(&b);
+  if (e != hipSuccess) return e;
+  (void)hipEventRecord(a, st);
+  e = launch();
+  (void)hipEventRecord(b, st);
+  d.pending[k].push_back({a, b});
+  return e;
+}
+
+hipError_t collect_times(Device& d) {
+  for (int k = 0; k < 3; ++k) {
+    for (auto& pr : d.pending[k]) {
+      hipError_t e = hipEventSynchronize(pr.second);
+      if (e != hipSuccess) return e;
+      float ms = 0;
+      e = hipEventElapsedTime(&ms, pr.first, pr.second);
+      if (e != hipSuccess) return e;
+      d.acc_ms[k] += ms;
+      d.launches[k] += 1;
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    d.pending[k].clear();
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+struct pbftv_ctx {
+  std::vector<std::unique_ptr<Device>> devs;
+  bool timing = false;
+};
+
+namespace {
+
+constexpr uint64_t kShardAlign = 512;
+
+struct Shard {
+  uint64_t lo, hi;
+};
+
+std::vector<Shard> plan_shards(uint64_t n, size_t ndev) {
+  std::vector<Shard> out;
+  if (n == 0) return out;
+  uint64_t per = (n + ndev - 1) / ndev;
+  per = (per + kShardAlign - 1) / kShardAlign * kShardAlign;
+  for (uint64_t lo = 0; lo < n; lo += per) out.push_back({lo, std::min(n, lo + per)});
+  return out;
+}
+
+// run fn(dev, shard) on every shard; one host thread per device when > 1 shard
+template <class Fn>
+int run_sharded(pbftv_ctx* ctx, uint64_t n, Fn fn) {
+  auto shards = plan_shards(n, ctx->devs.size());
+  if (shards.size() <= 1) {
+    return shards.empty() ? PBFTV_OK : fn(*ctx->devs[0], shards[0]);
+  }
+  std::vector<int> rc(shards.size(), PBFTV_OK);
+  std::vector<std::string> errs(shards.size());
+  std::vector<std::thread> th;
+  for (size_t s = 0; s < shards.size(); ++s) {
+    th.emplace_back([&, s] {
+      rc[s] = fn(*ctx->devs[s], shards[s]);
+      if (rc[s] != PBFTV_OK) errs[s] = g_last_error;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (size_t s = 0; s < shards.size(); ++s)
+    if (rc[s] != PBFTV_OK) return fail(rc[s], errs[s]);
+  return PBFTV_OK;
+}
+
+hipStream_t pick_stream(Device& d, void* stream) { return stream ? reinterpret_cast<hipStream_t>(stream) : d.stream; }
+
+}  // namespace
+
+extern "C" {
+
+const char* pbftv_strerror(int code) {
+  switch (code) {
+    case PBFTV_OK: return "ok";
+    case PBFTV_EINVAL: return "invalid argument";
+    case PBFTV_ENODEV: return "no usable gfx950 device";
+    case PBFTV_EDEVICE: return "HIP device error";
+    case PBFTV_ENOMEM: return "out of memory";
+    case PBFTV_ENOKEYS: return "no keys registered";
+    default: return "unknown error";
+  }
+}
+
+const char* pbftv_last_error(void) { return g_last_error.c_str(); }
+
+int pbftv_open(pbftv_ctx** out, uint32_t device_mask) {
+  if (!out) return fail(PBFTV_EINVAL, "out is null");
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(PBFTV_ENODEV, "no HIP devices visible");
+  auto ctx = std::make_unique<pbftv_ctx>();
+  for (int d = 0; d < count && d < 32; ++d) {
+    if (device_mask && !((device_mask >> d) & 1u)) continue;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) continue;  // the kernels are gfx950 code objects
+    auto dev = std::make_unique<Device>();
+    dev->id = d;
+    dev->timing = &ctx->timing;
+    HIP_TRY(hipSetDevice(d));
+    HIP_TRY(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
+    ctx->devs.push_back(std::move(dev));
+  }
+  if (ctx->devs.empty()) return fail(PBFTV_ENODEV, "no gfx950 device in device_mask");
+  *out = ctx.release();
+  return PBFTV_OK;
+}
+
+void pbftv_close(pbftv_ctx* ctx) {
+  if (!ctx) return;
+  for (auto& d : ctx->devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    (void)hipSetDevice(d->id);
+    (void)hipStreamSynchronize(d->stream);
+    (void)collect_times(*d);
+    for (DevBuf* b : {&d->tables, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag, &d->bitmap,
+                      &d->data, &d->offsets, &d->lengths, &d->order, &d->order_scratch, &d->digests, &d->expected,
+                      &d->shabits})
+      b->release();
+    (void)hipStreamDestroy(d->stream);
+  }
+  delete ctx;
+}
+
+int pbftv_device_count(const pbftv_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int pbftv_device_id(const pbftv_ctx* ctx, int i) {
+  if (!ctx || i < 0 || i >= (int)ctx->devs.size()) return -1;
+  return ctx->devs[i]->id;
+}
+
+int pbftv_reserve(pbftv_ctx* ctx, uint64_t n) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  for (auto& dp : ctx->devs) {
+    Device& d = *dp;
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(d.scal.ensure(n * 64));
+    HIP_TRY(d.flag.ensure(n));
+  }
+  return PBFTV_OK;
+}
+
+// ---------------------------------------------------------------- plumbing
+static Device* dev_of(pbftv_ctx* ctx, int dev) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return nullptr;
+  return ctx->devs[dev].get();
+}
+
+int pbftv_dev_alloc(pbftv_ctx* ctx, int dev, uint64_t bytes, void** out_ptr) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || !out_ptr) return fail(PBFTV_EINVAL, "bad context, device index or out pointer");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipMalloc(out_ptr, bytes ? bytes : 1));
+  return PBFTV_OK;
+}
+
+int pbftv_dev_free(pbftv_ctx* ctx, int dev, void* ptr) {
+  Device* d = dev_of(ctx, dev);
+  if (!d) return fail(PBFTV_EINVAL, "bad context or device index");
+  HIP_TRY(hipSetDevice(d->id));
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return PBFTV_OK;
+}
+
+int pbftv_memcpy_h2d(pbftv_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || (bytes && (!dst || !src))) return fail(PBFTV_EINVAL, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d->stream));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  return PBFTV_OK;
+}
+
+int pbftv_memcpy_d2h(pbftv_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || (bytes && (!dst || !src))) return fail(PBFTV_EINVAL, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d->stream));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  return PBFTV_OK;
+}
+
+int pbftv_memset_dev(pbftv_ctx* ctx, int dev, void* dst, int value, uint64_t bytes) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || (bytes && !dst)) return fail(PBFTV_EINVAL, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipMemsetAsync(dst, value, bytes, d->stream));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  return PBFTV_OK;
+}
+
+void* pbftv_stream(pbftv_ctx* ctx, int dev) {
+  Device* d = dev_of(ctx, dev);
+  return d ? reinterpret_cast<void*>(d->stream) : nullptr;
+}
+
+int pbftv_stream_sync(pbftv_ctx* ctx, int dev) {
+  Device* d = dev_of(ctx, dev);
+  if (!d) return fail(PBFTV_EINVAL, "bad context or device index");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  return PBFTV_OK;
+}
+
+int pbftv_set_kernel_timing(pbftv_ctx* ctx, int enable) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  ctx->timing = enable != 0;
+  return PBFTV_OK;
+}
+
+int pbftv_kernel_time_ms(pbftv_ctx* ctx, int dev, int kernel, double* out_ms, uint64_t* out_launches) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || kernel < 0 || kernel > 2) return fail(PBFTV_EINVAL, "bad argument");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(collect_times(*d));
+  if (out_ms) *out_ms = d->acc_ms[kernel];
+  if (out_launches) *out_launches = d->launches[kernel];
+  return PBFTV_OK;
+}
+
+int pbftv_reset_kernel_times(pbftv_ctx* ctx) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  for (auto& dp : ctx->devs) {
+    std::lock_guard<std::mutex> lk(dp->mu);
+    HIP_TRY(hipSetDevice(dp->id));
+    HIP_TRY(collect_times(*dp));
+    for (int k = 0; k < 3; ++k) {
+      dp->acc_ms[k] = 0;
+      dp->launches[k] = 0;
+    }
+  }
+  return PBFTV_OK;
+}
+
+// ---------------------------------------------------------------- keys
+int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid) {
+  if (!ctx || (k && !pub_xy)) return fail(PBFTV_EINVAL, "null argument");
+  // big-endian X||Y -> little-endian 32-bit words
+  std::vector<uint32_t> le((size_t)k * 16);
+  for (uint32_t j = 0; j < k; ++j) {
+    for (int c = 0; c < 2; ++c) {
+      const uint8_t* b = pub_xy + 64ull * j + 32 * c;
+      for (int w = 0; w < 8; ++w) {
+        const uint8_t* q = b + 4 * (7 - w);
+        le[16ull * j + 8 * c + w] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+      }
+    }
+  }
+  std::vector<uint32_t> valid(k ? k : 1, 0);
+  bool first = true;
+  for (auto& dp : ctx->devs) {
+    Device& d = *dp;
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    d.have_keys = false;
+    const size_t tbytes = (size_t)(k + 1) * pbftv::table_bytes_per_base();
+    HIP_TRY(d.tables.ensure(tbytes));
+    HIP_TRY(d.key_valid.ensure((size_t)(k ? k : 1) * 4));
+    DevBuf keys, scratch;
+    HIP_TRY(keys.ensure(le.size() * 4 + 4));
+    if (k) HIP_TRY(hipMemcpyAsync(keys.p, le.data(), le.size() * 4, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(scratch.ensure(pbftv::build_tables_scratch_bytes(k)));
+    HIP_TRY(pbftv::launch_build_tables(keys.as<uint32_t>(), k, d.tables.as<uint32_t>(), d.key_valid.as<uint32_t>(),
+                                       scratch.p, d.stream));
+    if (first && k) HIP_TRY(hipMemcpyAsync(valid.data(), d.key_valid.p, (size_t)k * 4, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    keys.release();
+    scratch.release();
+    d.nkeys = k;
+    d.have_keys = true;
+    first = false;
+  }
+  if (out_valid)
+    for (uint32_t j = 0; j < k; ++j) out_valid[j] = valid[j] ? 1 : 0;
+  return PBFTV_OK;
+}
+
+// ---------------------------------------------------------------- ecdsa
+static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d_sigs, const uint32_t* d_key_idx,
+                            uint64_t n, uint8_t* d_bitmap, hipStream_t st) {
+  if (!d.have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  HIP_TRY(d.scal.ensure(n * 64));
+  HIP_TRY(d.flag.ensure(n));
+  HIP_TRY(timed(d, PBFTV_K_ECDSA_SCALARS, st, [&] {
+    return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, d.scal.p,
+                                       d.flag.as<uint8_t>(), st);
+  }));
+  HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
+    return pbftv::launch_ecdsa_comb(d.scal.p, d.flag.as<uint8_t>(), d_sigs, d_key_idx, n, d.tables.as<uint32_t>(),
+                                    d_bitmap, st);
+  }));
+  return PBFTV_OK;
+}
+
+int pbftv_ecdsa_p256_verify_batch_dev(pbftv_ctx* ctx, int dev, const uint8_t* d_hashes, const uint8_t* d_sig_rs,
+                                      const uint32_t* d_key_idx, uint64_t n, uint8_t* d_bitmap, void* stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(PBFTV_EINVAL, "bad context or device index");
+  if (n && (!d_hashes || !d_sig_rs || !d_key_idx || !d_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
+  if (((uintptr_t)d_hashes | (uintptr_t)d_sig_rs) & 15u) return fail(PBFTV_EINVAL, "hashes/sigs must be 16-B aligned");
+  Device& d = *ctx->devs[dev];
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.id));
+  return verify_on_device(d, d_hashes, d_sig_rs, d_key_idx, n, d_bitmap, pick_stream(d, stream));
+}
+
+int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs,
+                                  const uint32_t* key_idx, uint64_t n, uint8_t* out_bitmap) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!hashes || !sig_rs || !key_idx || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
+  for (auto& dp : ctx->devs)
+    if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
+    const uint64_t m = s.hi - s.lo;
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(d.hashes.ensure(m * 32));
+    HIP_TRY(d.sigs.ensure(m * 64));
+    HIP_TRY(d.key_idx.ensure(m * 4));
+    HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
+    HIP_TRY(hipMemcpyAsync(d.hashes.p, hashes + 32 * s.lo, m * 32, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.sigs.p, sig_rs + 64 * s.lo, m * 64, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.key_idx.p, key_idx + s.lo, m * 4, hipMemcpyHostToDevice, d.stream));
+    int rc = verify_on_device(d, d.hashes.as<uint8_t>(), d.sigs.as<uint8_t>(), d.key_idx.as<uint32_t>(), m,
+                              d.bitmap.as<uint8_t>(), d.stream);
+    if (rc != PBFTV_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(out_bitmap + s.lo / 8, d.bitmap.p, (m + 7) / 8, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return PBFTV_OK;
+  });
+}
+
+int pbftv_qc_verify(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs, const uint32_t* key_idx, uint64_t n,
+                    uint32_t quorum, uint8_t* out_bitmap, uint64_t* out_accepted, int* out_quorum) {
+  std::vector<uint8_t> local;
+  uint8_t* bm = out_bitmap;
+  if (!bm) {
+    local.assign((n + 7) / 8 + 1, 0);
+    bm = local.data();
+  }
+  int rc = pbftv_ecdsa_p256_verify_batch(ctx, hashes, sig_rs, key_idx, n, bm);
+  if (rc != PBFTV_OK) return rc;
+  uint64_t cnt = 0;
+  for (uint64_t i = 0; i < n / 8; ++i) cnt += (uint64_t)__builtin_popcount(bm[i]);
+  if (n % 8) cnt += (uint64_t)__builtin_popcount(bm[n / 8] & ((1u << (n % 8)) - 1u));
+  if (out_accepted) *out_accepted = cnt;
+  if (out_quorum) *out_quorum = cnt >= quorum ? 1 : 0;
+  return PBFTV_OK;
+}
+
+// ---------------------------------------------------------------- sha256
+int pbftv_sha256_order_dev(pbftv_ctx* ctx, int dev, const uint32_t* d_lengths, uint64_t n, uint32_t* d_order,
+                           void* stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(PBFTV_EINVAL, "bad context or device index");
+  Device& d = *ctx->devs[dev];
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.id));
+  HIP_TRY(d.order_scratch.ensure(pbftv::sha256_order_scratch_bytes(n)));
+  HIP_TRY(pbftv::launch_sha256_order(d_lengths, n, d_order, d.order_scratch.p, pick_stream(d, stream)));
+  return PBFTV_OK;
+}
+
+int pbftv_sha256_batch_dev(pbftv_ctx* ctx, int dev, const uint8_t* d_data, const uint64_t* d_offsets,
+                           const uint32_t* d_lengths, const uint32_t* d_order, uint64_t n, uint8_t* d_digests,
+                           const uint8_t* d_expected, uint8_t* d_bitmap, void* stream) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(PBFTV_EINVAL, "bad context or device index");
+  if (n && (!d_data || !d_offsets || !d_lengths || !d_digests)) return fail(PBFTV_EINVAL, "null buffer");
+  if (d_expected && !d_bitmap) return fail(PBFTV_EINVAL, "expected given without bitmap");
+  Device& d = *ctx->devs[dev];
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.id));
+  hipStream_t st = pick_stream(d, stream);
+  HIP_TRY(timed(d, PBFTV_K_SHA256, st, [&] {
+    return pbftv::launch_sha256(d_data, d_offsets, d_lengths, d_order, n, d_digests, d_expected, d_bitmap, st);
+  }));
+  return PBFTV_OK;
+}
+
+static int sha_host(pbftv_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                    const uint8_t* expected, uint64_t n, uint8_t* out_digests, uint8_t* out_bitmap) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!offsets || !lengths)) return fail(PBFTV_EINVAL, "null buffer");
+  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
+    const uint64_t m = s.hi - s.lo;
+    // byte span of this shard, re-based offsets
+    uint64_t lo_b = UINT64_MAX, hi_b = 0;
+    for (uint64_t i = s.lo; i < s.hi; ++i) {
+      lo_b = std::min(lo_b, offsets[i]);
+      hi_b = std::max(hi_b, offsets[i] + lengths[i]);
+    }
+    if (hi_b > lo_b && !data) return fail(PBFTV_EINVAL, "data is null");
+    if (lo_b > hi_b) lo_b = hi_b;
+    std::vector<uint64_t> off(m);
+    for (uint64_t i = 0; i < m; ++i) off[i] = offsets[s.lo + i] - lo_b;
+    const uint64_t span = hi_b - lo_b;
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(d.data.ensure(span + 64));
+    HIP_TRY(d.offsets.ensure(m * 8));
+    HIP_TRY(d.lengths.ensure(m * 4));
+    HIP_TRY(d.order.ensure(m * 4));
+    HIP_TRY(d.digests.ensure(m * 32));
+    HIP_TRY(d.order_scratch.ensure(pbftv::sha256_order_scratch_bytes(m)));
+    if (span) HIP_TRY(hipMemcpyAsync(d.data.p, data + lo_b, span, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.offsets.p, off.data(), m * 8, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.lengths.p, lengths + s.lo, m * 4, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(pbftv::launch_sha256_order(d.lengths.as<uint32_t>(), m, d.order.as<uint32_t>(), d.order_scratch.p,
+                                       d.stream));
+    uint8_t* dexp = nullptr;
+    if (expected) {
+      HIP_TRY(d.expected.ensure(m * 32));
+      HIP_TRY(d.shabits.ensure((m + 31) / 32 * 4));
+      HIP_TRY(hipMemcpyAsync(d.expected.p, expected + 32 * s.lo, m * 32, hipMemcpyHostToDevice, d.stream));
+      dexp = d.expected.as<uint8_t>();
+    }
+    HIP_TRY(timed(d, PBFTV_K_SHA256, d.stream, [&] {
+      return pbftv::launch_sha256(d.data.as<uint8_t>(), d.offsets.as<uint64_t>(), d.lengths.as<uint32_t>(),
+                                  d.order.as<uint32_t>(), m, d.digests.as<uint8_t>(), dexp, d.shabits.as<uint8_t>(),
+                                  d.stream);
+    }));
+    if (out_digests)
+      HIP_TRY(hipMemcpyAsync(out_digests + 32 * s.lo, d.digests.p, m * 32, hipMemcpyDeviceToHost, d.stream));
+    if (expected)
+      HIP_TRY(hipMemcpyAsync(out_bitmap + s.lo / 8, d.shabits.p, (m + 7) / 8, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return PBFTV_OK;
+  });
+}
+
+int pbftv_sha256_batch(pbftv_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                       uint64_t n, uint8_t* out_digests) {
+  if (n && !out_digests) return fail(PBFTV_EINVAL, "out_digests is null");
+  return sha_host(ctx, data, offsets, lengths, nullptr, n, out_digests, nullptr);
+}
+
+int pbftv_digest_check_batch(pbftv_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                             const uint8_t* expected, uint64_t n, uint8_t* out_bitmap) {
+  if (n && (!expected || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
+  return sha_host(ctx, data, offsets, lengths, expected, n, nullptr, out_bitmap);
+}
+
+int pbftv_hash_hex(pbftv_ctx* ctx, const uint8_t* content, uint64_t len, char out_hex[65]) {
+  if (!out_hex || (len && !content)) return fail(PBFTV_EINVAL, "null buffer");
+  if (len > 0xFFFFFFFFull) return fail(PBFTV_EINVAL, "message longer than 4 GiB");
+  uint64_t off = 0;
+  uint32_t l = (uint32_t)len;
+  uint8_t dg[32];
+  int rc = pbftv_sha256_batch(ctx, content, &off, &l, 1, dg);
+  if (rc != PBFTV_OK) return rc;
+  static const char hx[] = "0123456789abcdef";  // encoding/hex: lowercase
+  for (int i = 0; i < 32; ++i) {
+    out_hex[2 * i] = hx[dg[i] >> 4];
+    out_hex[2 * i + 1] = hx[dg[i] & 15];
+  }
+  out_hex[64] = 0;
+  return PBFTV_OK;
+}
+
+int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
+                               const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
+                               const uint64_t* operation_off, const uint32_t* operation_len,
+                               const int64_t* sequence_ids, uint8_t* out_digests) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!timestamps || !client_id_off || !client_id_len || !operation_off || !operation_len || !sequence_ids ||
+            !out_digests))
+    return fail(PBFTV_EINVAL, "null buffer");
+  std::vector<uint8_t> buf;
+  std::vector<uint64_t> off(n);
+  std::vector<uint32_t> len(n);
+  buf.reserve(n * 112);
+  for (uint64_t i = 0; i < n; ++i) {
+    off[i] = buf.size();
+    pbftv::gojson::append_request(buf, timestamps[i], client_ids + client_id_off[i], client_id_len[i],
+                                  operations + operation_off[i], operation_len[i], sequence_ids[i]);
+    const uint64_t l = buf.size() - off[i];
+    if (l > 0xFFFFFFFFull) return fail(PBFTV_EINVAL, "preimage longer than 4 GiB");
+    len[i] = (uint32_t)l;
+  }
+  return pbftv_sha256_batch(ctx, buf.data(), off.data(), len.data(), n, out_digests);
+}
+
+int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const uint8_t req_digest[32], uint64_t n,
+                           const int64_t* view_ids, const int64_t* sequence_ids, const char* digest_got,
+                           const uint64_t* digest_got_off, const uint32_t* digest_got_len, uint8_t* out_bitmap) {
+  if (!req_digest || (n && (!view_ids || !sequence_ids || !digest_got_off || !digest_got_len || !out_bitmap)))
+    return fail(PBFTV_EINVAL, "null buffer");
+  static const char hx[] = "0123456789abcdef";
+  char want[64];
+  for (int i = 0; i < 32; ++i) {
+    want[2 * i] = hx[req_digest[i] >> 4];
+    want[2 * i + 1] = hx[req_digest[i] & 15];
+  }
+  std::memset(out_bitmap, 0, (n + 7) / 8);
+  for (uint64_t i = 0; i < n; ++i) {
+    bool ok = view_ids[i] == state_view_id;                                  // pbft_impl.go:178
+    if (ok && state_last_seq != -1) ok = state_last_seq < sequence_ids[i];    // pbft_impl.go:184-188
+    ok = ok && digest_got_len[i] == 64 && digest_got &&                       // pbft_impl.go:197 string compare
+         std::memcmp(digest_got + digest_got_off[i], want, 64) == 0;
+    if (ok) out_bitmap[i / 8] |= (uint8_t)(1u << (i % 8));
+  }
+  return PBFTV_OK;
+}
+
+uint64_t pbftv_gojson_request(int64_t timestamp, const char* client_id, uint64_t client_id_len, const char* operation,
+                              uint64_t operation_len, int64_t sequence_id, uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_request(b, timestamp, reinterpret_cast<const uint8_t*>(client_id), client_id_len,
+                                reinterpret_cast<const uint8_t*>(operation), operation_len, sequence_id);
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
+uint64_t pbftv_gojson_vote(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                           const char* node_id, uint64_t node_id_len, int64_t msg_type, uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_vote(b, view_id, sequence_id, reinterpret_cast<const uint8_t*>(digest), digest_len,
+                             reinterpret_cast<const uint8_t*>(node_id), node_id_len, msg_type);
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
+uint64_t pbftv_gojson_reply(int64_t view_id, int64_t timestamp, const char* client_id, uint64_t client_id_len,
+                            const char* node_id, uint64_t node_id_len, const char* result, uint64_t result_len,
+                            uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_reply(b, view_id, timestamp, reinterpret_cast<const uint8_t*>(client_id), client_id_len,
+                              reinterpret_cast<const uint8_t*>(node_id), node_id_len,
+                              reinterpret_cast<const uint8_t*>(result), result_len);
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
+uint64_t pbftv_gojson_preprepare(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                                 int has_request, int64_t req_timestamp, const char* req_client_id,
+                                 uint64_t req_client_id_len, const char* req_operation, uint64_t req_operation_len,
+                                 int64_t req_sequence_id, uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_preprepare(b, view_id, sequence_id, reinterpret_cast<const uint8_t*>(digest), digest_len,
+                                   has_request != 0, req_timestamp, reinterpret_cast<const uint8_t*>(req_client_id),
+                                   req_client_id_len, reinterpret_cast<const uint8_t*>(req_operation),
+                                   req_operation_len, req_sequence_id);
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
+}  // extern "C"

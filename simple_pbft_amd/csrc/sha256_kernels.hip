@@ -1,0 +1,198 @@
+// sha256_kernels.hip -- lane-per-message SHA-256 for gfx950.
+//
+// utils.Hash (utils/utils.go:13-17) = hex(SHA-256(content)); digest()
+// (pbft/consensus/pbft_impl.go:235-243) hashes the Go-JSON preimage.  Here one
+// lane owns one message: it streams the message's 64-B blocks from HBM with
+// dword loads re-aligned by v_alignbyte_b32 (messages sit at arbitrary byte
+// offsets), byte-swaps to big-endian and runs the fully unrolled 64-round
+// compression with v_alignbit_b32 rotates and v_bitop3_b32 for Ch / Maj /
+// three-way XORs.  Messages of mixed length are bucketed by block count
+// (k_len_hist / k_len_scan / k_len_scatter, a device counting sort) so the 64
+// lanes of a wave run the same number of blocks.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace pbftv {
+
+__device__ __constant__ static const uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+__device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    uint32_t wr;
+    if (r < 16) {
+      wr = w[r];
+    } else {
+      const uint32_t x = w[(r + 1) & 15], y = w[(r + 14) & 15];
+      const uint32_t s0 = rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3);
+      const uint32_t s1 = rotr(y, 17) ^ rotr(y, 19) ^ (y >> 10);
+      w[r & 15] += s0 + w[(r + 9) & 15] + s1;
+      wr = w[r & 15];
+    }
+    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + kK256[r] + wr;
+    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    const uint32_t mj = (a & b) | (c & (a | b));
+    const uint32_t t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+__device__ __forceinline__ uint32_t load_word(const uint32_t* q, uint64_t j) { return q[j]; }
+
+__global__ void __launch_bounds__(256) k_sha256(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
+                                                const uint32_t* __restrict__ lengths,
+                                                const uint32_t* __restrict__ order, uint64_t n,
+                                                uint8_t* __restrict__ digests, const uint8_t* __restrict__ expected,
+                                                uint32_t* __restrict__ bitmap32) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t m = order ? order[i] : i;
+  const uintptr_t a = (uintptr_t)(data + offsets[m]);
+  const uint32_t len = lengths[m];
+  const uint32_t sh = (uint32_t)(a & 3u);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a - sh);
+  uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  const uint32_t nfull = len >> 6;
+  uint32_t w[16];
+  for (uint32_t blk = 0; blk < nfull; ++blk) {
+    const uint32_t* qb = q + 16ull * blk;
+    uint32_t d[17];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d[j] = qb[j];
+    d[16] = sh ? qb[16] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[j + 1], d[j], sh));
+    compress(st, w);
+  }
+  // tail: rem bytes (0..63) + 0x80 + zeros + 64-bit bit length, in one or two blocks
+  const uint32_t rem = len - (nfull << 6);
+  const uint32_t* qt = q + 16ull * nfull;
+  uint32_t d[17];
+#pragma unroll
+  for (int j = 0; j < 17; ++j) d[j] = (4u * j < rem + sh) ? qt[j] : 0u;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t x = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);  // tail bytes 4j..4j+3, little-endian
+    const int v = (int)rem - 4 * j;                                  // message bytes remaining at this word
+    const uint32_t keep = v >= 4 ? 0xFFFFFFFFu : (v <= 0 ? 0u : ((1u << (8 * v)) - 1u));
+    x &= keep;
+    if (v >= 0 && v < 4) x |= 0x80u << (8 * v);
+    w[j] = __builtin_bswap32(x);
+  }
+  const uint64_t bits = (uint64_t)len << 3;
+  if (rem + 9 <= 64) {
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+    compress(st, w);
+  } else {
+    compress(st, w);
+#pragma unroll
+    for (int j = 0; j < 14; ++j) w[j] = 0;
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+    compress(st, w);
+  }
+  uint4* out = reinterpret_cast<uint4*>(digests + 32 * m);
+  const uint4 o0 = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                              __builtin_bswap32(st[3]));
+  const uint4 o1 = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                              __builtin_bswap32(st[7]));
+  out[0] = o0;
+  out[1] = o1;
+  if (expected) {
+    const uint4* ex = reinterpret_cast<const uint4*>(expected + 32 * m);
+    const uint4 e0 = ex[0], e1 = ex[1];
+    const bool eq = e0.x == o0.x && e0.y == o0.y && e0.z == o0.z && e0.w == o0.w && e1.x == o1.x && e1.y == o1.y &&
+                    e1.z == o1.z && e1.w == o1.w;
+    if (eq) atomicOr(bitmap32 + (m >> 5), 1u << (m & 31));
+  }
+}
+
+// ---- block-count bucketing (device counting sort) ----
+constexpr uint32_t kBuckets = 1024;
+
+__device__ __forceinline__ uint32_t bucket_of(uint32_t len) {
+  const uint32_t nb = (len + 8u) / 64u + 1u;  // compression calls for this message
+  return nb >= kBuckets ? kBuckets - 1 : nb;
+}
+
+__global__ void __launch_bounds__(256) k_len_hist(const uint32_t* __restrict__ lengths, uint64_t n,
+                                                  uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kBuckets];
+  for (uint32_t b = threadIdx.x; b < kBuckets; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&h[bucket_of(lengths[i])], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kBuckets; b += blockDim.x)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// exclusive scan in descending bucket order (longest messages first), one block of kBuckets threads
+__global__ void __launch_bounds__(1024) k_len_scan(uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s[kBuckets];
+  const uint32_t t = threadIdx.x;
+  s[t] = hist[kBuckets - 1 - t];
+  __syncthreads();
+  for (uint32_t off = 1; off < kBuckets; off <<= 1) {
+    const uint32_t v = t >= off ? s[t - off] : 0u;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  const uint32_t incl = s[t];
+  hist[kBuckets - 1 - t] = incl - hist[kBuckets - 1 - t];  // exclusive start of bucket
+}
+
+__global__ void __launch_bounds__(256) k_len_scatter(const uint32_t* __restrict__ lengths, uint64_t n,
+                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ order) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t pos = atomicAdd(&cursor[bucket_of(lengths[i])], 1u);
+  order[pos] = (uint32_t)i;
+}
+
+size_t sha256_order_scratch_bytes(uint64_t) { return kBuckets * sizeof(uint32_t); }
+
+hipError_t launch_sha256_order(const uint32_t* lengths, uint64_t n, uint32_t* order, void* scratch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(scratch);
+  hipError_t e = hipMemsetAsync(hist, 0, kBuckets * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  uint64_t blocks = (n + 255) / 256;
+  const uint32_t hb = (uint32_t)(blocks < 2048 ? blocks : 2048);
+  hipLaunchKernelGGL(k_len_hist, dim3(hb), dim3(256), 0, st, lengths, n, hist);
+  hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(kBuckets), 0, st, hist);
+  hipLaunchKernelGGL(k_len_scatter, dim3((uint32_t)blocks), dim3(256), 0, st, lengths, n, hist, order);
+  return hipGetLastError();
+}
+
+hipError_t launch_sha256(const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, const uint32_t* order,
+                         uint64_t n, uint8_t* digests, const uint8_t* expected, uint8_t* bitmap, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (expected) {
+    hipError_t e = hipMemsetAsync(bitmap, 0, ((n + 31) / 32) * 4, st);
+    if (e != hipSuccess) return e;
+  }
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)blocks), dim3(256), 0, st, data, offsets, lengths, order, n, digests,
+                     expected, reinterpret_cast<uint32_t*>(bitmap));
+  return hipGetLastError();
+}
+
+}  // namespace pbftv

@@ -1,0 +1,387 @@
+"""ctypes binding of the C ABI in include/pbftv.h (libpbftv.so, built in-tree).
+
+This is plumbing for tests and bench.py: the product is the shared library.
+Loading fails loudly if libpbftv.so is missing, and ``Verifier()`` fails with
+``PbftvError(PBFTV_ENODEV)`` when no gfx950 GPU is visible -- there is no
+CPU fallback anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpbftv.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "pbftv.h")
+
+PBFTV_OK = 0
+PBFTV_EINVAL = -1
+PBFTV_ENODEV = -2
+PBFTV_EDEVICE = -3
+PBFTV_ENOMEM = -4
+PBFTV_ENOKEYS = -5
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+
+_lib = None
+
+
+class PbftvError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"pbftv error {code}: {msg}")
+        self.code = code
+
+
+def lib() -> ctypes.CDLL:
+    """Load libpbftv.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "or `make -C simple_pbft_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "pbftv_open": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_uint32]),
+        "pbftv_close": (None, [_vp]),
+        "pbftv_device_count": (ctypes.c_int, [_vp]),
+        "pbftv_device_id": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "pbftv_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+        "pbftv_last_error": (ctypes.c_char_p, []),
+        "pbftv_reserve": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+        "pbftv_dev_alloc": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(_vp)]),
+        "pbftv_dev_free": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+        "pbftv_memcpy_h2d": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_uint64]),
+        "pbftv_memcpy_d2h": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_uint64]),
+        "pbftv_memset_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint64]),
+        "pbftv_stream": (_vp, [_vp, ctypes.c_int]),
+        "pbftv_stream_sync": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "pbftv_set_kernel_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "pbftv_kernel_time_ms": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_uint64)]),
+        "pbftv_reset_kernel_times": (ctypes.c_int, [_vp]),
+        "pbftv_hash_hex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_char_p]),
+        "pbftv_sha256_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+        "pbftv_digest_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+        "pbftv_sha256_batch_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp,
+                                                  _vp, _vp]),
+        "pbftv_sha256_order_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_uint64, _vp, _vp]),
+        "pbftv_gojson_request": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p,
+                                                   ctypes.c_uint64, ctypes.c_int64, _vp, ctypes.c_uint64]),
+        "pbftv_gojson_vote": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64,
+                                                ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int64, _vp,
+                                                ctypes.c_uint64]),
+        "pbftv_gojson_reply": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64,
+                                                 ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                                                 _vp, ctypes.c_uint64]),
+        "pbftv_gojson_preprepare": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p,
+                                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_int64, ctypes.c_char_p,
+                                                      ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                                                      ctypes.c_int64, _vp, ctypes.c_uint64]),
+        "pbftv_digest_request_batch": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                      _vp]),
+        "pbftv_verify_msg_batch": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _vp, ctypes.c_uint64, _vp, _vp,
+                                                  _vp, _vp, _vp, _vp]),
+        "pbftv_register_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+        "pbftv_ecdsa_p256_verify_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+        "pbftv_ecdsa_p256_verify_batch_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint64, _vp,
+                                                             _vp]),
+        "pbftv_qc_verify": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp,
+                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def header_symbols() -> list[str]:
+    """Every function declared in include/pbftv.h."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pbftv_[a-z0-9_]+)\s*\(", text)))
+
+
+def _ptr(a) -> int | None:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"]
+        return a.ctypes.data
+    if isinstance(a, (bytes, bytearray)):
+        return ctypes.cast(ctypes.c_char_p(bytes(a)), ctypes.c_void_p).value
+    return int(a)
+
+
+def _check(rc: int):
+    if rc != PBFTV_OK:
+        L = lib()
+        raise PbftvError(rc, (L.pbftv_last_error() or b"").decode() or L.pbftv_strerror(rc).decode())
+
+
+def bitmap_to_bool(bm: np.ndarray, n: int) -> np.ndarray:
+    return np.unpackbits(np.asarray(bm, dtype=np.uint8), bitorder="little")[:n].astype(bool)
+
+
+# ---------------------------------------------------------------- host-only helpers (no GPU)
+def gojson_request(ts: int, client_id: bytes, operation: bytes, seq: int) -> bytes:
+    L = lib()
+    n = L.pbftv_gojson_request(ts, client_id, len(client_id), operation, len(operation), seq, None, 0)
+    buf = np.zeros(max(n, 1), np.uint8)
+    L.pbftv_gojson_request(ts, client_id, len(client_id), operation, len(operation), seq, buf.ctypes.data, n)
+    return buf[:n].tobytes()
+
+
+def gojson_vote(view: int, seq: int, digest: bytes, node_id: bytes, msg_type: int) -> bytes:
+    L = lib()
+    n = L.pbftv_gojson_vote(view, seq, digest, len(digest), node_id, len(node_id), msg_type, None, 0)
+    buf = np.zeros(max(n, 1), np.uint8)
+    L.pbftv_gojson_vote(view, seq, digest, len(digest), node_id, len(node_id), msg_type, buf.ctypes.data, n)
+    return buf[:n].tobytes()
+
+
+def gojson_reply(view: int, ts: int, client_id: bytes, node_id: bytes, result: bytes) -> bytes:
+    L = lib()
+    args = (view, ts, client_id, len(client_id), node_id, len(node_id), result, len(result))
+    n = L.pbftv_gojson_reply(*args, None, 0)
+    buf = np.zeros(max(n, 1), np.uint8)
+    L.pbftv_gojson_reply(*args, buf.ctypes.data, n)
+    return buf[:n].tobytes()
+
+
+def gojson_preprepare(view: int, seq: int, digest: bytes, req) -> bytes:
+    L = lib()
+    if req is None:
+        args = (view, seq, digest, len(digest), 0, 0, b"", 0, b"", 0, 0)
+    else:
+        ts, cid, op, rseq = req
+        args = (view, seq, digest, len(digest), 1, ts, cid, len(cid), op, len(op), rseq)
+    n = L.pbftv_gojson_preprepare(*args, None, 0)
+    buf = np.zeros(max(n, 1), np.uint8)
+    L.pbftv_gojson_preprepare(*args, buf.ctypes.data, n)
+    return buf[:n].tobytes()
+
+
+def verify_msg_batch(state_view: int, state_last_seq: int, req_digest: bytes, view_ids, seq_ids,
+                     digests_got: list[bytes]) -> np.ndarray:
+    n = len(digests_got)
+    blob = b"".join(digests_got)
+    off = np.zeros(n, np.uint64)
+    ln = np.array([len(d) for d in digests_got], np.uint32)
+    if n:
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    v = np.ascontiguousarray(view_ids, np.int64)
+    s = np.ascontiguousarray(seq_ids, np.int64)
+    bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+    blob_arr = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
+    rd = np.frombuffer(req_digest, np.uint8).copy()
+    _check(lib().pbftv_verify_msg_batch(state_view, state_last_seq, rd.ctypes.data, n, v.ctypes.data, s.ctypes.data,
+                                        blob_arr.ctypes.data, off.ctypes.data, ln.ctypes.data, bm.ctypes.data))
+    return bitmap_to_bool(bm, n)
+
+
+# ---------------------------------------------------------------- GPU context
+K_ECDSA_SCALARS = 0
+K_ECDSA_COMB = 1
+K_SHA256 = 2
+
+
+class DeviceBuffer:
+    """A pbftv_dev_alloc allocation on one of the context's devices."""
+
+    def __init__(self, ver: "Verifier", dev: int, ptr: int, nbytes: int):
+        self.ver, self.dev, self.ptr, self.nbytes = ver, dev, ptr, nbytes
+
+    def to_host(self, nbytes: int | None = None, dtype=np.uint8) -> np.ndarray:
+        nb = self.nbytes if nbytes is None else nbytes
+        out = np.zeros(max(nb, 1), np.uint8)
+        if nb:
+            _check(self.ver._L.pbftv_memcpy_d2h(self.ver._h, self.dev, out.ctypes.data, self.ptr, nb))
+        return out[:nb].view(dtype)
+
+    def zero(self):
+        _check(self.ver._L.pbftv_memset_dev(self.ver._h, self.dev, self.ptr, 0, self.nbytes))
+
+    def free(self):
+        if self.ptr and self.ver._h is not None:
+            _check(self.ver._L.pbftv_dev_free(self.ver._h, self.dev, self.ptr))
+        self.ptr = 0
+
+
+class Verifier:
+    """A pbftv_ctx: the GPUs in device_mask (0 = all visible gfx950 devices)."""
+
+    def __init__(self, device_mask: int = 0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        _check(self._L.pbftv_open(ctypes.byref(h), device_mask))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.pbftv_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def device_count(self) -> int:
+        return self._L.pbftv_device_count(self._h)
+
+    def device_id(self, i: int) -> int:
+        return self._L.pbftv_device_id(self._h, i)
+
+    def reserve(self, n: int):
+        _check(self._L.pbftv_reserve(self._h, n))
+
+    # ---- device memory plumbing (no torch: torch bundles its own HIP runtime)
+    def alloc(self, dev: int, nbytes: int) -> "DeviceBuffer":
+        p = ctypes.c_void_p()
+        _check(self._L.pbftv_dev_alloc(self._h, dev, nbytes, ctypes.byref(p)))
+        return DeviceBuffer(self, dev, p.value, nbytes)
+
+    def to_device(self, dev: int, arr: np.ndarray, pad: int = 0) -> "DeviceBuffer":
+        arr = np.ascontiguousarray(arr)
+        buf = self.alloc(dev, arr.nbytes + pad)
+        if arr.nbytes:
+            _check(self._L.pbftv_memcpy_h2d(self._h, dev, buf.ptr, arr.ctypes.data, arr.nbytes))
+        if pad:
+            _check(self._L.pbftv_memset_dev(self._h, dev, buf.ptr + arr.nbytes, 0, pad))
+        return buf
+
+    def stream(self, dev: int) -> int:
+        return self._L.pbftv_stream(self._h, dev)
+
+    def sync(self, dev: int):
+        _check(self._L.pbftv_stream_sync(self._h, dev))
+
+    def set_kernel_timing(self, on: bool):
+        _check(self._L.pbftv_set_kernel_timing(self._h, 1 if on else 0))
+
+    def kernel_time_ms(self, dev: int, kernel: int):
+        ms = ctypes.c_double()
+        cnt = ctypes.c_uint64()
+        _check(self._L.pbftv_kernel_time_ms(self._h, dev, kernel, ctypes.byref(ms), ctypes.byref(cnt)))
+        return ms.value, cnt.value
+
+    def reset_kernel_times(self):
+        _check(self._L.pbftv_reset_kernel_times(self._h))
+
+    # ---- sha256 / digests
+    def hash_hex(self, content: bytes) -> str:
+        out = ctypes.create_string_buffer(65)
+        arr = np.frombuffer(content, np.uint8) if content else np.zeros(1, np.uint8)
+        _check(self._L.pbftv_hash_hex(self._h, arr.ctypes.data, len(content), out))
+        return out.value.decode()
+
+    @staticmethod
+    def pack(messages: list[bytes]):
+        lengths = np.array([len(m) for m in messages], np.uint32)
+        offsets = np.zeros(len(messages), np.uint64)
+        if len(messages):
+            offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+        blob = np.frombuffer(b"".join(messages), np.uint8) if sum(map(len, messages)) else np.zeros(1, np.uint8)
+        return np.ascontiguousarray(blob), offsets, lengths
+
+    def sha256_batch(self, data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
+        n = len(lengths)
+        out = np.zeros((max(n, 1), 32), np.uint8)
+        data = np.ascontiguousarray(data, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        lengths = np.ascontiguousarray(lengths, np.uint32)
+        _check(self._L.pbftv_sha256_batch(self._h, data.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, n,
+                                          out.ctypes.data))
+        return out[:n]
+
+    def digest_check_batch(self, data, offsets, lengths, expected: np.ndarray) -> np.ndarray:
+        n = len(lengths)
+        bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+        data = np.ascontiguousarray(data, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        lengths = np.ascontiguousarray(lengths, np.uint32)
+        expected = np.ascontiguousarray(expected, np.uint8)
+        _check(self._L.pbftv_digest_check_batch(self._h, data.ctypes.data, offsets.ctypes.data, lengths.ctypes.data,
+                                                expected.ctypes.data, n, bm.ctypes.data))
+        return bitmap_to_bool(bm, n)
+
+    def digest_request_batch(self, requests) -> np.ndarray:
+        """requests: list of (timestamp, clientID bytes, operation bytes, sequenceID)."""
+        n = len(requests)
+        ts = np.array([r[0] for r in requests], np.int64)
+        seq = np.array([r[3] for r in requests], np.int64)
+        cid_blob, cid_off, cid_len = self.pack([r[1] for r in requests])
+        op_blob, op_off, op_len = self.pack([r[2] for r in requests])
+        out = np.zeros((max(n, 1), 32), np.uint8)
+        _check(self._L.pbftv_digest_request_batch(self._h, n, ts.ctypes.data, cid_blob.ctypes.data,
+                                                  cid_off.ctypes.data, cid_len.ctypes.data, op_blob.ctypes.data,
+                                                  op_off.ctypes.data, op_len.ctypes.data, seq.ctypes.data,
+                                                  out.ctypes.data))
+        return out[:n]
+
+    # ---- ecdsa
+    def register_keys(self, pub_xy: np.ndarray) -> np.ndarray:
+        pub_xy = np.ascontiguousarray(pub_xy, np.uint8).reshape(-1, 64)
+        k = pub_xy.shape[0]
+        valid = np.zeros(max(k, 1), np.uint8)
+        _check(self._L.pbftv_register_keys(self._h, pub_xy.ctypes.data, k, valid.ctypes.data))
+        return valid[:k].astype(bool)
+
+    def verify_batch(self, hashes: np.ndarray, sig_rs: np.ndarray, key_idx: np.ndarray) -> np.ndarray:
+        hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)
+        sig_rs = np.ascontiguousarray(sig_rs, np.uint8).reshape(-1, 64)
+        key_idx = np.ascontiguousarray(key_idx, np.uint32)
+        n = hashes.shape[0]
+        assert sig_rs.shape[0] == n and key_idx.shape[0] == n
+        bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+        _check(self._L.pbftv_ecdsa_p256_verify_batch(self._h, hashes.ctypes.data, sig_rs.ctypes.data,
+                                                     key_idx.ctypes.data, n, bm.ctypes.data))
+        return bitmap_to_bool(bm, n)
+
+    def verify_batch_dev(self, dev: int, d_hashes: int, d_sigs: int, d_key_idx: int, n: int, d_bitmap: int,
+                         stream: int | None = None):
+        _check(self._L.pbftv_ecdsa_p256_verify_batch_dev(self._h, dev, d_hashes, d_sigs, d_key_idx, n, d_bitmap,
+                                                         stream))
+
+    def sha256_order_dev(self, dev: int, d_lengths: int, n: int, d_order: int, stream: int | None = None):
+        _check(self._L.pbftv_sha256_order_dev(self._h, dev, d_lengths, n, d_order, stream))
+
+    def sha256_batch_dev(self, dev: int, d_data: int, d_offsets: int, d_lengths: int, d_order: int | None, n: int,
+                         d_digests: int, d_expected: int | None = None, d_bitmap: int | None = None,
+                         stream: int | None = None):
+        _check(self._L.pbftv_sha256_batch_dev(self._h, dev, d_data, d_offsets, d_lengths, d_order, n, d_digests,
+                                              d_expected, d_bitmap, stream))
+
+    def qc_verify(self, hashes, sig_rs, key_idx, quorum: int):
+        hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)
+        sig_rs = np.ascontiguousarray(sig_rs, np.uint8).reshape(-1, 64)
+        key_idx = np.ascontiguousarray(key_idx, np.uint32)
+        n = hashes.shape[0]
+        bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+        acc = ctypes.c_uint64()
+        ok = ctypes.c_int()
+        _check(self._L.pbftv_qc_verify(self._h, hashes.ctypes.data, sig_rs.ctypes.data, key_idx.ctypes.data, n,
+                                       quorum, bm.ctypes.data, ctypes.byref(acc), ctypes.byref(ok)))
+        return bitmap_to_bool(bm, n), int(acc.value), bool(ok.value)

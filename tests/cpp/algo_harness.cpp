@@ -1,0 +1,125 @@
+// algo_harness.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Compiles the GPU kernels' arithmetic headers (simple_pbft_amd/csrc/fe29.h,
+// p256_algo.h) with g++ so that tests/test_algo_cpu.py can check, on the
+// CPU of this container, the exact limb arithmetic, bounds and verify
+// pipeline that the HIP kernels run.  It is never linked into or loaded by
+// the product library (simple_pbft_amd/libpbftv.so), which runs this code on
+// the GPU only.
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../simple_pbft_amd/csrc/p256_algo.h"
+
+using namespace pbftv;
+
+extern "C" {
+
+void h_fe_mul(const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  fe x, y, z;
+  memcpy(x.v, a, 36); memcpy(y.v, b, 36);
+  fe_mul(z, x, y);
+  memcpy(r, z.v, 36);
+}
+void h_fe_sqr(const uint32_t* a, uint32_t* r) {
+  fe x, z;
+  memcpy(x.v, a, 36);
+  fe_sqr(z, x);
+  memcpy(r, z.v, 36);
+}
+void h_fe_sub(const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  fe x, y, z;
+  memcpy(x.v, a, 36); memcpy(y.v, b, 36);
+  fe_sub(z, x, y);
+  memcpy(r, z.v, 36);
+}
+void h_fe_mul_small(const uint32_t* a, uint32_t k, uint32_t* r) {
+  fe x, z;
+  memcpy(x.v, a, 36);
+  fe_mul_small(z, x, k);
+  memcpy(r, z.v, 36);
+}
+void h_fe_canon(const uint32_t* a, uint32_t* r) {
+  fe x, z;
+  memcpy(x.v, a, 36);
+  fe_canon(z, x);
+  memcpy(r, z.v, 36);
+}
+void h_fn_mul(const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  fe x, y, z;
+  memcpy(x.v, a, 36); memcpy(y.v, b, 36);
+  fn_mul(z, x, y);
+  memcpy(r, z.v, 36);
+}
+void h_fe_from_words(const uint32_t* w, uint32_t* r) {
+  fe z;
+  fe_from_words(z, w);
+  memcpy(r, z.v, 36);
+}
+void h_fe_to_words(const uint32_t* a, uint32_t* w) {
+  fe x;
+  memcpy(x.v, a, 36);
+  fe_to_words(w, x);
+}
+int h_scalars(const uint32_t* e, const uint32_t* r, const uint32_t* s, uint32_t* u1, uint32_t* u2) {
+  return ecdsa_scalars(e, r, s, u1, u2) ? 1 : 0;
+}
+
+static void be32_to_le_words(const uint8_t* b, uint32_t* w) {
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* p = b + 4 * (7 - i);
+    w[i] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  }
+}
+
+// Build the comb table of base (x, y) [big-endian 64 B]; returns key validity.
+int h_build_table(const uint8_t* pub_xy, uint32_t* table) {
+  uint32_t xw[8], yw[8];
+  be32_to_le_words(pub_xy, xw);
+  be32_to_le_words(pub_xy + 32, yw);
+  fe xm, ym;
+  if (!key_check(xw, yw, xm, ym)) {
+    memset(table, 0, kTableBytes);
+    return 0;
+  }
+  std::vector<fe> scratch(kScratchSlots);
+  for (int w = 0; w < kWindows; ++w) {
+    build_window(table + (uint64_t)w * kEntries * kEntryWords, w, xm, ym,
+                 [&](int slot, const fe& v) { scratch[slot] = v; },
+                 [&](int slot, fe& v) { v = scratch[slot]; });
+  }
+  return 1;
+}
+
+void h_build_g_table(uint32_t* table) {
+  fe gx, gy;
+  fe_set(gx, kGxMont);
+  fe_set(gy, kGyMont);
+  std::vector<fe> scratch(kScratchSlots);
+  for (int w = 0; w < kWindows; ++w) {
+    build_window(table + (uint64_t)w * kEntries * kEntryWords, w, gx, gy,
+                 [&](int slot, const fe& v) { scratch[slot] = v; },
+                 [&](int slot, fe& v) { v = scratch[slot]; });
+  }
+}
+
+// Full pipeline on one signature given prebuilt tables.
+int h_verify(const uint8_t* hash, const uint8_t* rs, const uint32_t* gtab, const uint32_t* qtab, int key_valid) {
+  if (!key_valid) return 0;
+  uint32_t e[8], r[8], s[8], u1[8], u2[8];
+  be32_to_le_words(hash, e);
+  be32_to_le_words(rs, r);
+  be32_to_le_words(rs + 32, s);
+  if (!ecdsa_scalars(e, r, s, u1, u2)) return 0;
+  jac A, B;
+  bool aok = comb_mult(A, u1, [&](int win, int idx, uint32_t* out) {
+    memcpy(out, gtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64);
+  });
+  bool bok = comb_mult(B, u2, [&](int win, int idx, uint32_t* out) {
+    memcpy(out, qtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64);
+  });
+  return ecdsa_final(A, aok, B, bok, r) ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,230 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the
+committed golden fixtures.  Bit-exact for every digest and every accept bit."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import fixture_arrays, oracle_sign_pool
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ver():
+    from simple_pbft_amd import Verifier
+    v = Verifier()
+    yield v
+    v.close()
+
+
+# ------------------------------------------------------------------ SHA-256
+def test_sha256_fixtures(ver, sha_fixtures):
+    msgs, want = [], []
+    for v in sha_fixtures:
+        if "msg" in v:
+            msgs.append(bytes.fromhex(v["msg"]))
+        else:
+            msgs.append(bytes.fromhex(v["msg_repeat"]["byte"]) * v["msg_repeat"]["count"])
+        want.append(v["digest"])
+    blob, off, ln = ver.pack(msgs)
+    got = ver.sha256_batch(blob, off, ln)
+    assert [g.tobytes().hex() for g in got] == want
+
+
+def test_sha256_random_unaligned(ver):
+    rng = np.random.default_rng(7)
+    n = 3000
+    lengths = rng.integers(0, 8193, n).astype(np.uint32)
+    lengths[:130] = np.arange(130)  # every tail shape
+    gaps = rng.integers(0, 7, n)
+    offsets = np.zeros(n, np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(gaps[i])
+        offsets[i] = pos
+        pos += int(lengths[i])
+    data = np.frombuffer(rng.bytes(pos + 16), np.uint8).copy()
+    got = ver.sha256_batch(data, offsets, lengths)
+    for i in range(n):
+        m = data[offsets[i]:offsets[i] + lengths[i]].tobytes()
+        assert got[i].tobytes() == hashlib.sha256(m).digest(), (i, lengths[i], offsets[i])
+
+
+def test_sha256_empty_batch_and_empty_message(ver):
+    assert ver.sha256_batch(np.zeros(1, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32)).shape == (0, 32)
+    assert ver.hash_hex(b"") == hashlib.sha256(b"").hexdigest()
+
+
+def test_digest_check(ver):
+    rng = np.random.default_rng(3)
+    msgs = [rng.bytes(int(l)) for l in rng.integers(0, 300, 777)]
+    blob, off, ln = ver.pack(msgs)
+    exp = np.array([list(hashlib.sha256(m).digest()) for m in msgs], np.uint8)
+    flip = rng.random(len(msgs)) < 0.3
+    exp[flip, 5] ^= 0x40
+    got = ver.digest_check_batch(blob, off, ln, exp)
+    assert (got == ~flip).all()
+
+
+def test_hash_hex_and_request_digests(ver, digest_kats):
+    """utils.Hash / digest(*RequestMsg) on the reference's own logged requests."""
+    reqs = []
+    for r in digest_kats["requests"] + digest_kats["escapes"]:
+        pre = bytes.fromhex(r["preimage"])
+        assert ver.hash_hex(pre) == r["digest"]
+        reqs.append((r["timestamp"], bytes.fromhex(r["clientID"]), bytes.fromhex(r["operation"]), r["sequenceID"]))
+    got = ver.digest_request_batch(reqs)
+    want = [r["digest"] for r in digest_kats["requests"] + digest_kats["escapes"]]
+    assert [g.tobytes().hex() for g in got] == want
+
+
+def test_sha256_dev_api(ver):
+    rng = np.random.default_rng(11)
+    msgs = [rng.bytes(int(l)) for l in rng.integers(256, 4097, 2048)]
+    blob, off, ln = ver.pack(msgs)
+    n = len(msgs)
+    d_data = ver.to_device(0, blob, pad=16)
+    d_off = ver.to_device(0, off)
+    d_len = ver.to_device(0, ln)
+    d_ord = ver.alloc(0, 4 * n)
+    d_dig = ver.alloc(0, 32 * n)
+    exp = np.array([list(hashlib.sha256(m).digest()) for m in msgs], np.uint8)
+    exp[::3, 0] ^= 1
+    d_exp = ver.to_device(0, exp)
+    d_bm = ver.alloc(0, (n + 31) // 32 * 4)
+    ver.sha256_order_dev(0, d_len.ptr, n, d_ord.ptr)
+    ver.sha256_batch_dev(0, d_data.ptr, d_off.ptr, d_len.ptr, d_ord.ptr, n, d_dig.ptr, d_exp.ptr, d_bm.ptr)
+    ver.sync(0)
+    order = d_ord.to_host(dtype=np.uint32)
+    assert sorted(order.tolist()) == list(range(n))
+    nb = (ln.astype(np.int64) + 8) // 64 + 1
+    assert (np.diff(nb[order]) <= 0).all(), "order must group by descending block count"
+    got = d_dig.to_host().reshape(-1, 32)
+    for i, m in enumerate(msgs):
+        assert got[i].tobytes() == hashlib.sha256(m).digest()
+    bits = np.unpackbits(d_bm.to_host(), bitorder="little")[:n].astype(bool)
+    assert (bits == (np.arange(n) % 3 != 0)).all()
+    for b in (d_data, d_off, d_len, d_ord, d_dig, d_exp, d_bm):
+        b.free()
+
+
+# ------------------------------------------------------------------ ECDSA
+def test_register_keys_validity(ver, ecdsa_fixtures):
+    keys, *_ = fixture_arrays(ecdsa_fixtures)
+    valid = ver.register_keys(keys)
+    assert valid.tolist() == [k["valid"] for k in ecdsa_fixtures["keys"]]
+
+
+def test_ecdsa_fixtures(ver, ecdsa_fixtures):
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    ver.register_keys(keys)
+    got = ver.verify_batch(hashes, sigs, kidx)
+    bad = [(ecdsa_fixtures["vectors"][i]["kind"], bool(got[i])) for i in np.nonzero(got != expect)[0]]
+    assert not bad, bad
+
+
+def test_ecdsa_fixtures_every_alignment(ver, ecdsa_fixtures):
+    """Same vectors at every position of a wave / bitmap byte."""
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    ver.register_keys(keys)
+    for shift in (1, 7, 63):
+        h = np.concatenate([hashes[:shift], hashes])
+        s = np.concatenate([sigs[:shift], sigs])
+        k = np.concatenate([kidx[:shift], kidx])
+        e = np.concatenate([expect[:shift], expect])
+        assert (ver.verify_batch(h, s, k) == e).all()
+
+
+def test_ecdsa_random_vs_oracle(ver, oracle_lib):
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=16, per_key=64, seed=99)
+    rng = np.random.default_rng(5)
+    n = len(kidx)
+    # corrupt a third of them in assorted ways
+    c = rng.integers(0, 6, n)
+    sel = rng.random(n) < 0.33
+    for i in np.nonzero(sel)[0]:
+        kind = c[i]
+        if kind == 0:
+            sigs[i, rng.integers(0, 32)] ^= 1 << rng.integers(0, 8)
+        elif kind == 1:
+            sigs[i, 32 + rng.integers(0, 32)] ^= 1 << rng.integers(0, 8)
+        elif kind == 2:
+            hashes[i, rng.integers(0, 32)] ^= 1 << rng.integers(0, 8)
+        elif kind == 3:
+            kidx[i] = (kidx[i] + 1) % 16
+        elif kind == 4:
+            sigs[i, :32] = 0
+        else:
+            sigs[i, 32:] = 0xFF
+    ver.register_keys(keys)
+    got = ver.verify_batch(hashes, sigs, kidx)
+    want = np.zeros((n + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n].astype(bool)
+    assert (got == want).all()
+    assert want.sum() > n // 2
+
+
+def test_ecdsa_large_tiled_property(ver, oracle_lib):
+    """262,144 signatures (tiles of an oracle-signed pool) with 1 % corrupted at
+    known positions: the accept bitmap must be exactly the complement of the
+    corruption mask (size-independent property; multi-shard / many waves)."""
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=8, per_key=64, seed=123)
+    reps = 262144 // len(kidx)
+    H = np.tile(hashes, (reps, 1))
+    S = np.tile(sigs, (reps, 1))
+    K = np.tile(kidx, reps)
+    rng = np.random.default_rng(8)
+    bad = rng.random(len(K)) < 0.01
+    idx = np.nonzero(bad)[0]
+    S[idx, 63] ^= 1
+    ver.register_keys(keys)
+    got = ver.verify_batch(H, S, K)
+    assert (got == ~bad).all()
+
+
+def test_ecdsa_no_keys_and_out_of_range(ecdsa_fixtures):
+    from simple_pbft_amd import PBFTV_ENOKEYS, PbftvError, Verifier
+    with Verifier() as v:
+        keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+        with pytest.raises(PbftvError) as ei:
+            v.verify_batch(hashes[:3], sigs[:3], kidx[:3])
+        assert ei.value.code == PBFTV_ENOKEYS
+        v.register_keys(keys[:2])
+        k = np.full(len(kidx), 5, np.uint32)
+        assert not v.verify_batch(hashes, sigs, k).any()
+
+
+def test_qc_verify(ver, oracle_lib):
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=4, per_key=3, seed=4)
+    ver.register_keys(keys)
+    bm, acc, ok = ver.qc_verify(hashes, sigs, kidx, quorum=3)
+    assert bm.all() and acc == 12 and ok
+    sigs[:10, 40] ^= 1
+    bm, acc, ok = ver.qc_verify(hashes, sigs, kidx, quorum=3)
+    assert acc == 2 and not ok and bm.tolist() == [False] * 10 + [True] * 2
+
+
+def test_ecdsa_dev_api(ver, ecdsa_fixtures):
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    ver.register_keys(keys)
+    n = len(kidx)
+    dh = ver.to_device(0, hashes)
+    ds = ver.to_device(0, sigs)
+    dk = ver.to_device(0, kidx)
+    db = ver.alloc(0, (n + 7) // 8)
+    ver.set_kernel_timing(True)
+    ver.reset_kernel_times()
+    ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
+    ver.sync(0)
+    ms, cnt = ver.kernel_time_ms(0, 1)
+    ver.set_kernel_timing(False)
+    assert cnt == 1 and ms > 0
+    got = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
+    assert (got == expect).all()
+    for b in (dh, ds, dk, db):
+        b.free()
