@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Benchmark: ECDSA-P256 signature verifies/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n SIGS_PER_RANK]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (BASELINE.json configs[3]): 1,048,576
+signatures per rank over a 100-key table, 1 % corrupted evenly across the 8
+corruption classes; synthetic (OpenSSL-signed, tools/synth.py).  One "step" =
+one pass of the verify path (scalar kernel + comb kernel) over the rank's
+whole batch, inputs already resident in HBM.  Multi-GPU: one process per GPU,
+each verifying its own shard -- no collective on the data path; torch.distributed
+(gloo, CPU) is used only for the barrier and the max-over-ranks time, so torch
+never touches the GPU (it bundles its own HIP runtime).
+
+Also reported on rank 0: p50 quorum-certificate verify latency (host submit ->
+bitmap on host, configs[1]/[2] certificate sizes), the roofline of the
+dominant kernel (HIP-event kernel durations from the timed region), and the
+CPU baseline (oracle port, multi-threaded, bounded sample) beside an OpenSSL
+stand-in.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import synth  # noqa: E402
+from simple_pbft_amd import Verifier  # noqa: E402
+from simple_pbft_amd.pbftv import K_ECDSA_COMB, K_ECDSA_SCALARS  # noqa: E402
+
+METRIC = "sig verifies/sec at 1/2/4/8 MI355X; p50 quorum-cert verify latency"
+
+# ---- algorithmic work per verify (DESIGN.md "Roofline"): limb MACs ----------
+# One MAC = one 29x29-bit limb product accumulated into a 64-bit column
+# (one v_mad_u64_u32).  fe_mul 81, fe_sqr 45, fn_mul 81 + 81 (n-reduction).
+N_ORDER = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+FE_MUL, FE_SQR, FN_MUL = 81, 45, 162
+MADD = 7 * FE_MUL + 4 * FE_SQR                     # madd-2007-bl
+JADD = 12 * FE_MUL + 4 * FE_SQR                    # add-2007-bl (final complete add)
+# windows 0..31 nonzero w.p. 255/256, window 32 w.p. ~1/2; first nonzero is a load
+ADDS_PER_COMB = 32 * 255 / 256 + 0.5 - 1
+MACS_COMB = 2 * ADDS_PER_COMB * MADD + JADD + (FE_SQR + 2 * FE_MUL)
+MACS_SCALARS = (1 + 256 + bin(N_ORDER - 2).count("1") + 2) * FN_MUL
+# v_mad_u64_u32 issue peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz (4-cycle wave64 issue);
+# measured 30.9 T lane-ops/s in profiles/r01_valu_microbench.txt
+MAD_PEAK = 256 * 4 * 16 * 2.4e9
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+class Dist:
+    def __init__(self, ws):
+        self.ws = ws
+        self.dist = None
+        if ws > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int):
+    pub, H, S, K = synth.qc(n_keys, sigs, seed)
+    ver.register_keys(pub)
+    for _ in range(20):
+        ver.qc_verify(H, S, K, quorum=sigs)
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        _, acc, ok = ver.qc_verify(H, S, K, quorum=sigs)
+        ts.append(time.perf_counter() - t0)
+        assert ok and acc == sigs
+    return float(np.percentile(ts, 50) * 1e6), float(np.percentile(ts, 99) * 1e6)
+
+
+def cpu_baseline(pub, H, S, K, sample: int):
+    """Oracle port (oracle/p256_ref.c, Go crypto/ecdsa restatement) on host threads."""
+    so = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(so):
+        return None
+    L = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    L.oracle_ecdsa_p256_verify_batch.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_int]
+    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 cores
+    h, s, k = (np.ascontiguousarray(a[:sample]) for a in (H, S, K))
+    bm = np.zeros((sample + 7) // 8, np.uint8)
+    t0 = time.perf_counter()
+    L.oracle_ecdsa_p256_verify_batch(h.ctypes.data, s.ctypes.data, k.ctypes.data, sample, pub.ctypes.data, len(pub),
+                                     bm.ctypes.data, threads)
+    dt = time.perf_counter() - t0
+    return {"value": sample / dt, "unit": "verifies/s", "cores": threads, "kind": "port",
+            "sample": f"first {sample} signatures of the config-4 batch (oracle/p256_ref.c, {threads} pthreads)",
+            "_bitmap": bm}
+
+
+def openssl_standin(pub, H, S, K, sample: int):
+    """OpenSSL ECDSA_do_verify, single thread (SURVEY.md §8(d)(ii) stand-in); scaled x cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        from oracle import openssl_xcheck
+    except Exception:
+        return None
+    t0 = time.perf_counter()
+    for i in range(sample):
+        kk = pub[K[i]]
+        openssl_xcheck.ecdsa_verify(H[i].tobytes(), int.from_bytes(S[i, :32].tobytes(), "big"),
+                                    int.from_bytes(S[i, 32:].tobytes(), "big"),
+                                    int.from_bytes(kk[:32].tobytes(), "big"), int.from_bytes(kk[32:].tobytes(), "big"))
+    dt = time.perf_counter() - t0
+    return {"value_per_core": sample / dt, "unit": "verifies/s", "cores": 1,
+            "note": "OpenSSL 3 ECDSA_do_verify via ctypes incl. key/sig object setup per call"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per rank")
+    ap.add_argument("--keys", type=int, default=100)
+    ap.add_argument("--no-extras", action="store_true", help="skip QC latency and CPU baseline")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    d = Dist(ws)
+    ver = Verifier(device_mask=1 << local)
+    n = args.n
+    pub, H, S, K, ok = synth.config4(n, n_keys=args.keys, seed=0x50424654 + rank)
+    valid = ver.register_keys(pub)
+    assert valid.all()
+    dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
+    db = ver.alloc(0, (n + 7) // 8)
+    ver.reserve(n)
+
+    def step():
+        ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
+
+    for _ in range(args.warmup):
+        step()
+    ver.sync(0)
+    got = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
+    check = bool((got == ok).all())
+
+    ver.set_kernel_timing(True)
+    ver.reset_kernel_times()
+    d.barrier()
+    ver.sync(0)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ver.sync(0)
+    d.barrier()
+    elapsed = time.perf_counter() - t0
+    comb_ms, comb_cnt = ver.kernel_time_ms(0, K_ECDSA_COMB)
+    scal_ms, scal_cnt = ver.kernel_time_ms(0, K_ECDSA_SCALARS)
+    ver.set_kernel_timing(False)
+    t_max = d.max(elapsed)
+    all_ok = d.sum(0.0 if check else 1.0) == 0.0
+    total = n * ws * args.steps
+    value = total / t_max
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": ws, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (OpenSSL-signed P-256 votes, tools/synth.py)",
+        "config": {"workload": f"config4: {n} ECDSA-P256 sigs per rank, {args.keys}-key table, 1% corrupted "
+                               "(8 classes)", "global_batch": n * ws, "keys": args.keys,
+                   "parallelism": f"shard{ws} (independent per-GPU batches, no collective)"},
+        "check": "pass" if all_ok else "FAIL",
+    }
+    if rank == 0:
+        comb_avg = comb_ms / max(comb_cnt, 1) * 1e-3
+        scal_avg = scal_ms / max(scal_cnt, 1) * 1e-3
+        kern = {
+            "ecdsa_comb": {"avg_ms": comb_avg * 1e3, "macs_per_verify": MACS_COMB,
+                           "achieved_tmacs": n * MACS_COMB / comb_avg / 1e12},
+            "ecdsa_scalars": {"avg_ms": scal_avg * 1e3, "macs_per_verify": MACS_SCALARS,
+                              "achieved_tmacs": n * MACS_SCALARS / scal_avg / 1e12},
+        }
+        dom = "ecdsa_comb" if comb_avg >= scal_avg else "ecdsa_scalars"
+        ach = kern[dom]["achieved_tmacs"]
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+        out["roofline"] = {"bound": "valu", "kernel": dom, "achieved": ach, "peak": MAD_PEAK / 1e12,
+                           "unit": "TMAC/s (v_mad_u64_u32 limb MACs)", "frac": ach * 1e12 / MAD_PEAK,
+                           "traffic": traffic}
+        out["kernels"] = kern
+        if not args.no_extras and ws == 1:
+            p50_4, p99_4 = qc_latency(ver, 4, 3, 2000, 11)
+            p50_100, p99_100 = qc_latency(ver, 100, 67, 1000, 12)
+            out["qc_latency_us"] = {"p50_n4_3sigs": p50_4, "p99_n4_3sigs": p99_4, "p50_n100_67sigs": p50_100,
+                                    "p99_n100_67sigs": p99_100,
+                                    "definition": "host submit -> accept bitmap + quorum on host, pbftv_qc_verify"}
+            cb = cpu_baseline(pub, H, S, K, sample=32768)
+            if cb is not None:
+                bm = cb.pop("_bitmap")
+                cpu_bits = np.unpackbits(bm, bitorder="little")[:32768].astype(bool)
+                cb["agrees_with_gpu"] = bool((cpu_bits == got[:32768]).all())
+                out["cpu_baseline"] = cb
+                out["gpu_vs_cpu"] = value / cb["value"]
+            ost = openssl_standin(pub, H, S, K, sample=4000)
+            if ost is not None:
+                out["cpu_openssl_standin"] = ost
+        print(json.dumps(out), flush=True)
+    for b in (dh, ds, dk, db):
+        b.free()
+    ver.close()
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

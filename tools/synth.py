@@ -1,0 +1,180 @@
+"""Synthetic signed-vote workloads for bench.py.
+
+Signatures are produced with OpenSSL 3 libcrypto (ECDSA_do_sign) -- neither the
+product library nor the oracle -- so the benchmark verifies signatures made by
+an independent implementation.  Keys are derived deterministically from the
+seed; nonces are OpenSSL's own (random), so signatures differ run to run while
+the accept/reject pattern is fixed by construction:
+
+    corrupt(i) for i in a seeded 1 % subset, split evenly over the 8 classes of
+    SURVEY.md §8(c): flip r, flip s, flip hash, wrong key, r=0, s=0, r=n, s>=n.
+"""
+from __future__ import annotations
+
+import ctypes
+import ctypes.util
+import hashlib
+
+import numpy as np
+
+NID_P256 = 415
+N_ORDER = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+CLASSES = ["flip r", "flip s", "flip hash", "wrong key", "r=0", "s=0", "r=n", "s>=n"]
+
+_L = None
+
+
+def _lib():
+    global _L
+    if _L is None:
+        L = ctypes.CDLL(ctypes.util.find_library("crypto") or "libcrypto.so.3")
+        vp = ctypes.c_void_p
+        L.EC_KEY_new_by_curve_name.restype = vp
+        L.EC_KEY_new_by_curve_name.argtypes = [ctypes.c_int]
+        L.EC_KEY_get0_group.restype = vp
+        L.EC_KEY_get0_group.argtypes = [vp]
+        L.EC_KEY_set_private_key.argtypes = [vp, vp]
+        L.EC_KEY_set_public_key.argtypes = [vp, vp]
+        L.EC_POINT_new.restype = vp
+        L.EC_POINT_new.argtypes = [vp]
+        L.EC_POINT_free.argtypes = [vp]
+        L.EC_POINT_mul.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.EC_POINT_get_affine_coordinates.argtypes = [vp, vp, vp, vp, vp]
+        L.BN_new.restype = vp
+        L.BN_free.argtypes = [vp]
+        L.BN_bin2bn.restype = vp
+        L.BN_bin2bn.argtypes = [ctypes.c_char_p, ctypes.c_int, vp]
+        L.BN_bn2binpad.argtypes = [vp, ctypes.c_char_p, ctypes.c_int]
+        L.ECDSA_do_sign.restype = vp
+        L.ECDSA_do_sign.argtypes = [ctypes.c_char_p, ctypes.c_int, vp]
+        L.ECDSA_SIG_get0_r.restype = vp
+        L.ECDSA_SIG_get0_r.argtypes = [vp]
+        L.ECDSA_SIG_get0_s.restype = vp
+        L.ECDSA_SIG_get0_s.argtypes = [vp]
+        L.ECDSA_SIG_free.argtypes = [vp]
+        L.EC_KEY_free.argtypes = [vp]
+        _L = L
+    return _L
+
+
+class Signer:
+    """n_keys deterministic P-256 keys (OpenSSL EC_KEY objects)."""
+
+    def __init__(self, n_keys: int, seed: int):
+        L = _lib()
+        self.keys = []
+        self.pub = np.zeros((n_keys, 64), np.uint8)
+        for j in range(n_keys):
+            d = int.from_bytes(hashlib.sha256(b"pbft-key:%d:%d" % (seed, j)).digest(), "big") % (N_ORDER - 1) + 1
+            k = L.EC_KEY_new_by_curve_name(NID_P256)
+            grp = L.EC_KEY_get0_group(k)
+            db = d.to_bytes(32, "big")
+            bn = L.BN_bin2bn(db, 32, None)
+            L.EC_KEY_set_private_key(k, bn)
+            pt = L.EC_POINT_new(grp)
+            L.EC_POINT_mul(grp, pt, bn, None, None, None)
+            L.EC_KEY_set_public_key(k, pt)
+            bx, by = L.BN_new(), L.BN_new()
+            L.EC_POINT_get_affine_coordinates(grp, pt, bx, by, None)
+            xb, yb = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+            L.BN_bn2binpad(bx, xb, 32)
+            L.BN_bn2binpad(by, yb, 32)
+            self.pub[j] = np.frombuffer(xb.raw + yb.raw, np.uint8)
+            for b in (bx, by, bn):
+                L.BN_free(b)
+            L.EC_POINT_free(pt)
+            self.keys.append(k)
+
+    def sign(self, h: bytes, j: int) -> bytes:
+        L = _lib()
+        sig = L.ECDSA_do_sign(h, 32, self.keys[j])
+        rb, sb = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+        L.BN_bn2binpad(L.ECDSA_SIG_get0_r(sig), rb, 32)
+        L.BN_bn2binpad(L.ECDSA_SIG_get0_s(sig), sb, 32)
+        L.ECDSA_SIG_free(sig)
+        return rb.raw + sb.raw
+
+    def close(self):
+        L = _lib()
+        for k in self.keys:
+            L.EC_KEY_free(k)
+        self.keys = []
+
+
+def signed_pool(n_keys: int, pool: int, seed: int):
+    """pool distinct (hash, sig, key) triples, keys round-robin."""
+    s = Signer(n_keys, seed)
+    rng = np.random.default_rng(seed)
+    hashes = np.frombuffer(rng.bytes(32 * pool), np.uint8).reshape(pool, 32).copy()
+    kidx = (np.arange(pool) % n_keys).astype(np.uint32)
+    sigs = np.zeros((pool, 64), np.uint8)
+    for i in range(pool):
+        sigs[i] = np.frombuffer(s.sign(hashes[i].tobytes(), int(kidx[i])), np.uint8)
+    pub = s.pub.copy()
+    s.close()
+    return pub, hashes, sigs, kidx
+
+
+def corrupt(hashes, sigs, kidx, n_keys: int, frac: float, seed: int):
+    """Corrupt a seeded `frac` subset in place, evenly over CLASSES; returns the expected accept mask."""
+    n = len(kidx)
+    rng = np.random.default_rng(seed ^ 0x5A5A)
+    m = int(round(n * frac))
+    idx = rng.choice(n, m, replace=False)
+    nb = N_ORDER.to_bytes(32, "big")
+    for t, i in enumerate(idx):
+        c = t % 8
+        if c == 0:
+            sigs[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif c == 1:
+            sigs[i, 32 + rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif c == 2:
+            hashes[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+        elif c == 3:
+            kidx[i] = (kidx[i] + 1 + rng.integers(0, n_keys - 1)) % n_keys
+        elif c == 4:
+            sigs[i, :32] = 0
+        elif c == 5:
+            sigs[i, 32:] = 0
+        elif c == 6:
+            sigs[i, :32] = np.frombuffer(nb, np.uint8)
+        else:
+            sigs[i, 32:] = 0xFF
+    ok = np.ones(n, bool)
+    ok[idx] = False
+    return ok
+
+
+def config4(n: int, n_keys: int = 100, pool: int = 65536, seed: int = 0x50424654, frac: float = 0.01):
+    """n sigs over an n_keys table, `frac` corrupted.
+    The distinct pool is tiled to n (every tile holds distinct hashes/sigs)."""
+    pub, h, s, k = signed_pool(n_keys, min(pool, n), seed)
+    reps = -(-n // len(k))
+    H = np.tile(h, (reps, 1))[:n].copy()
+    S = np.tile(s, (reps, 1))[:n].copy()
+    K = np.tile(k, reps)[:n].copy()
+    ok = corrupt(H, S, K, n_keys, frac, seed)
+    return pub, H, S, K, ok
+
+
+def qc(n_keys: int, sigs_per_qc: int, seed: int):
+    """One quorum certificate: sigs_per_qc votes over one digest from distinct replicas."""
+    s = Signer(n_keys, seed)
+    h = hashlib.sha256(b"qc-digest:%d" % seed).digest()
+    H = np.tile(np.frombuffer(h, np.uint8), (sigs_per_qc, 1))
+    K = (np.arange(sigs_per_qc) % n_keys).astype(np.uint32)
+    S = np.stack([np.frombuffer(s.sign(h, int(j)), np.uint8) for j in K])
+    pub = s.pub.copy()
+    s.close()
+    return pub, H, S, K
+
+
+def sha_config5(n: int, lo: int = 256, hi: int = 4096, seed: int = 0x50424654):
+    """n messages of uniform random length in [lo, hi] B, random bytes."""
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(lo, hi + 1, n).astype(np.uint32)
+    offsets = np.zeros(n, np.uint64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.uint64)
+    total = int(lengths.sum())
+    data = rng.integers(0, 256, total + 64, dtype=np.uint8)
+    return data, offsets, lengths
