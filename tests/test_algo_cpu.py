@@ -1,0 +1,154 @@
+"""The GPU kernels' arithmetic, compiled for the CPU (tests/cpp/algo_harness.cpp),
+checked against Python big integers and the oracle: limb bounds of every
+field operation (the invariants fe29.h documents), and the full verify
+pipeline (scalars -> comb tables -> final complete addition) on every golden
+vector.  This is test infrastructure: the product runs this code only on the GPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, fixture_arrays, oracle_sign_pool
+
+P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
+N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+R = 1 << 261
+M29 = (1 << 29) - 1
+TABLE_WORDS = 33 * 128 * 16
+M_BOUND = int(1.172 * 2 ** 256)
+L_BOUND = int(2.344 * 2 ** 256)
+
+
+@pytest.fixture(scope="module")
+def H():
+    d = os.path.join(ROOT, "tests", "cpp")
+    so = os.path.join(d, "libalgo_harness.so")
+    src = os.path.join(d, "algo_harness.cpp")
+    hdrs = [os.path.join(ROOT, "simple_pbft_amd", "csrc", f) for f in ("fe29.h", "p256_algo.h", "p256_consts.h")]
+    if not os.path.exists(so) or any(os.path.getmtime(h) > os.path.getmtime(so) for h in hdrs + [src]):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", so, src], check=True)
+    return ctypes.CDLL(so)
+
+
+def limbs(v):
+    return (ctypes.c_uint32 * 9)(*[(v >> (29 * i)) & M29 for i in range(9)])
+
+
+def val(l):
+    return sum(int(x) << (29 * i) for i, x in enumerate(l))
+
+
+def rand_l_type(rng):
+    """A lazily-added (L-type) input: limbs < 2^30, value < 2.344 * 2^256."""
+    while True:
+        l = [int(rng.choice([rng.integers(0, 1 << 30), (1 << 30) - 1, 0, 1 << 29])) for _ in range(9)]
+        l[8] = int(rng.integers(0, 1 << 26))
+        if val(l) < L_BOUND:
+            return (ctypes.c_uint32 * 9)(*l), val(l)
+
+
+def test_fe_mul_sqr_sub_bounds(H):
+    rng = np.random.default_rng(1)
+    out = (ctypes.c_uint32 * 9)()
+    edge = [0, 1, P - 1, P, P + 1, 2 ** 256 - 1, M_BOUND - 1]
+    for it in range(4000):
+        if it < len(edge) ** 2:
+            a, b = edge[it // len(edge)], edge[it % len(edge)]
+            la, lb = limbs(a), limbs(b)
+        elif it % 2:
+            a, b = int(rng.integers(0, 2 ** 62)) ** 4 % P, int(rng.integers(0, 2 ** 62)) ** 4 % P
+            la, lb = limbs(a), limbs(b)
+        else:
+            (la, a), (lb, b) = rand_l_type(rng), rand_l_type(rng)
+        H.h_fe_mul(la, lb, out)
+        v = val(out)
+        assert v % P == a * b * pow(R, -1, P) % P
+        assert all(x < (1 << 29) for x in out) and v < M_BOUND
+        H.h_fe_sqr(la, out)
+        v = val(out)
+        assert v % P == a * a * pow(R, -1, P) % P and all(x < (1 << 29) for x in out) and v < M_BOUND
+        H.h_fe_sub(la, lb, out)
+        v = val(out)
+        assert v % P == (a - b) % P and all(x < (1 << 29) for x in out) and v < 2 ** 256 + 2 ** 231
+        H.h_fe_canon(limbs(a % M_BOUND), out)
+        assert val(out) == (a % M_BOUND) % P
+
+
+def test_fe_mul_small_and_words(H):
+    rng = np.random.default_rng(2)
+    out = (ctypes.c_uint32 * 9)()
+    w = (ctypes.c_uint32 * 8)()
+    for _ in range(500):
+        a = int.from_bytes(rng.bytes(32), "big") % M_BOUND
+        for k in (2, 3, 4):
+            H.h_fe_mul_small(limbs(a), k, out)
+            assert val(out) % P == k * a % P and val(out) < 2 ** 256 + 2 ** 231
+        b = a % (2 ** 256)
+        H.h_fe_to_words(limbs(b), w)
+        assert sum(int(x) << (32 * i) for i, x in enumerate(w)) == b
+        H.h_fe_from_words(w, out)
+        assert val(out) == b
+
+
+def test_fn_mul_and_scalars(H):
+    rng = np.random.default_rng(3)
+    out = (ctypes.c_uint32 * 9)()
+    for _ in range(2000):
+        a = int.from_bytes(rng.bytes(32), "big")
+        b = int.from_bytes(rng.bytes(32), "big")
+        H.h_fn_mul(limbs(a), limbs(b), out)
+        assert val(out) % N == a * b * pow(R, -1, N) % N and val(out) < 2 * N
+    W = ctypes.c_uint32 * 8
+    for _ in range(50):
+        e, r, s = (int.from_bytes(rng.bytes(32), "big") for _ in range(3))
+        r, s = r % N or 1, s % N or 1
+        u1, u2 = W(), W()
+        ok = H.h_scalars(W(*[(e >> 32 * i) & 0xFFFFFFFF for i in range(8)]),
+                         W(*[(r >> 32 * i) & 0xFFFFFFFF for i in range(8)]),
+                         W(*[(s >> 32 * i) & 0xFFFFFFFF for i in range(8)]), u1, u2)
+        assert ok
+        w = pow(s, -1, N)
+        assert sum(int(x) << 32 * i for i, x in enumerate(u1)) == e * w % N
+        assert sum(int(x) << 32 * i for i, x in enumerate(u2)) == r * w % N
+
+
+def _tables(H, keys):
+    g = (ctypes.c_uint32 * TABLE_WORDS)()
+    H.h_build_g_table(g)
+    tabs, valid = [], []
+    for k in keys:
+        t = (ctypes.c_uint32 * TABLE_WORDS)()
+        valid.append(H.h_build_table(k.tobytes(), t))
+        tabs.append(t)
+    return g, tabs, valid
+
+
+def test_pipeline_on_golden_vectors(H, ecdsa_fixtures):
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    g, tabs, valid = _tables(H, keys)
+    assert [bool(v) for v in valid] == [k["valid"] for k in ecdsa_fixtures["keys"]]
+    for i in range(len(kidx)):
+        k = int(kidx[i])
+        got = H.h_verify(hashes[i].tobytes(), sigs[i].tobytes(), g, tabs[k], valid[k]) if k < len(tabs) else 0
+        assert bool(got) == expect[i], ecdsa_fixtures["vectors"][i]["kind"]
+
+
+def test_pipeline_random_vs_oracle(H, oracle_lib):
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=4, per_key=40, seed=5)
+    rng = np.random.default_rng(6)
+    n = len(kidx)
+    flip = rng.random(n) < 0.4
+    sigs[flip, 50] ^= 0x10
+    g, tabs, valid = _tables(H, keys)
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n,
+                                              keys.ctypes.data, len(keys), bm.ctypes.data, 4)
+    want = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    for i in range(n):
+        got = H.h_verify(hashes[i].tobytes(), sigs[i].tobytes(), g, tabs[kidx[i]], valid[kidx[i]])
+        assert bool(got) == want[i]
+    assert (want == ~flip).all()
