@@ -50,10 +50,27 @@ JADD = 12 * FE_MUL + 4 * FE_SQR                    # add-2007-bl (final complete
 # windows 0..31 nonzero w.p. 255/256, window 32 w.p. ~1/2; first nonzero is a load
 ADDS_PER_COMB = 32 * 255 / 256 + 0.5 - 1
 MACS_COMB = 2 * ADDS_PER_COMB * MADD + JADD + (FE_SQR + 2 * FE_MUL)
-MACS_SCALARS = (1 + 256 + bin(N_ORDER - 2).count("1") + 2) * FN_MUL
+INV_N = 292                                         # fn_inv_mont addition chain (p256_algo.h)
+
+
+def macs_scalars(k: int) -> float:
+    """k signatures per lane share one inversion (Montgomery's trick, p256_kernels.hip)."""
+    per_sig = 7 if k > 1 else 4
+    return (per_sig + INV_N / k) * FN_MUL
 # v_mad_u64_u32 issue peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz (4-cycle wave64 issue);
 # measured 30.9 T lane-ops/s in profiles/r01_valu_microbench.txt
 MAD_PEAK = 256 * 4 * 16 * 2.4e9
+
+
+def scalar_batch(n: int) -> int:
+    """Mirror of pbftv::scalar_batch (p256_kernels.hip)."""
+    e = os.environ.get("PBFTV_SCALAR_BATCH")
+    if e in ("1", "2", "4", "8", "16"):
+        return int(e)
+    lanes, k = 256 * 4 * 64 * 2, 1
+    while k < 16 and n >= 2 * k * lanes:
+        k *= 2
+    return k
 
 
 def dist_env():
@@ -211,11 +228,13 @@ def main():
     if rank == 0:
         comb_avg = comb_ms / max(comb_cnt, 1) * 1e-3
         scal_avg = scal_ms / max(scal_cnt, 1) * 1e-3
+        kb = scalar_batch(n)
+        ms = macs_scalars(kb)
         kern = {
             "ecdsa_comb": {"avg_ms": comb_avg * 1e3, "macs_per_verify": MACS_COMB,
                            "achieved_tmacs": n * MACS_COMB / comb_avg / 1e12},
-            "ecdsa_scalars": {"avg_ms": scal_avg * 1e3, "macs_per_verify": MACS_SCALARS,
-                              "achieved_tmacs": n * MACS_SCALARS / scal_avg / 1e12},
+            "ecdsa_scalars": {"avg_ms": scal_avg * 1e3, "macs_per_verify": ms, "sigs_per_lane": kb,
+                              "achieved_tmacs": n * ms / scal_avg / 1e12},
         }
         dom = "ecdsa_comb" if comb_avg >= scal_avg else "ecdsa_scalars"
         ach = kern[dom]["achieved_tmacs"]

@@ -19,7 +19,7 @@
 // Value/limb invariants (checked by tests/test_algo_cpu.py on CPU).  A Montgomery
 // product satisfies out < a*b/2^261 + p + 2^225, whose fixed point gives:
 //   M-type (fe_mul/fe_sqr output): limbs < 2^29, value < 1.172 * 2^256
-//   N-type (fe_sub/fe_norm/fe_mul_small output): limbs < 2^29, value < 2^256 + 2^231
+//   N-type (fe_sub/fe_norm/fe_mul_small output): limbs < 2^29, value < 2^256 + 2^237
 //   L-type (fe_add of two M/N values): limbs < 2^30, value < 2.344 * 2^256
 //   fe_mul/fe_sqr inputs: any two of M/N/L (limbs < 2^30 keep every column < 2^64)
 //   fe_sub inputs: any of M/N/L (a - b + 4p > 0 since b < 2.344 * 2^256 < 4p)
@@ -96,12 +96,30 @@ PBFTV_HD void fe_fold_signed(fe& r, int32_t d[9]) {
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = (uint32_t)d[i];
 }
 
-// r = a - b (mod p) as N-type.
+// Single-pass normalise + fold of signed limbs d (|d_i| < 2^31 - 2^26).  The
+// part of limb 8 at and above bit 24 (value bits >= 256) is folded in BEFORE
+// the carry pass via 2^256 == 2^224 - 2^192 - 2^96 + 1 (mod p), with the
+// quotient taken 4 low (floor((d_8 - 4) / 2^24)) so limb 8 ends in
+// [4, 2^24 + 4) before carries and, since the carry arriving from limb 7 is in
+// [-4, 4], >= 0 after.  The result is therefore a non-negative N-type
+// representative for ANY sign of the input value: no multiple of p needs to
+// be added for subtraction.
+PBFTV_HD void fe_fold_carry(fe& r, int32_t d[9]) {
+  const int32_t top = (d[8] - 4) >> 24;
+  d[8] -= top << 24;
+  d[0] += top;
+  d[3] -= top << 9;
+  d[6] -= top << 18;
+  d[7] += top << 21;
+  fe_carry_signed(d);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = (uint32_t)d[i];
+}
+
+// r = a - b (mod p) as N-type (a, b any of M/N/L: |a_i - b_i| < 2^30).
 PBFTV_HD void fe_sub(fe& r, const fe& a, const fe& b) {
   int32_t d[9];
-  PBFTV_UNROLL for (int i = 0; i < 9; ++i) d[i] = (int32_t)(a.v[i] + kP4[i]) - (int32_t)b.v[i];
-  fe_carry_signed(d);
-  fe_fold_signed(r, d);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) d[i] = (int32_t)a.v[i] - (int32_t)b.v[i];
+  fe_fold_carry(r, d);
 }
 
 // lazy r = a + b (L-type: only as fe_mul/fe_sqr/fe_sub input)
@@ -109,20 +127,18 @@ PBFTV_HD void fe_add(fe& r, const fe& a, const fe& b) {
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
 }
 
-// r = k * a mod p (k <= 4, a limbs < 2^29) as N-type
+// r = k * a mod p (1 <= k <= 3, a limbs < 2^29) as N-type
 PBFTV_HD void fe_mul_small(fe& r, const fe& a, uint32_t k) {
   int32_t d[9];
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) d[i] = (int32_t)(a.v[i] * k);
-  fe_carry_signed(d);
-  fe_fold_signed(r, d);
+  fe_fold_carry(r, d);
 }
 
 // normalise an L-type value to N-type
 PBFTV_HD void fe_norm(fe& r, const fe& a) {
   int32_t d[9];
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) d[i] = (int32_t)a.v[i];
-  fe_carry_signed(d);
-  fe_fold_signed(r, d);
+  fe_fold_carry(r, d);
 }
 
 // r = 2p - a, lazily (a canonical or N-type with limbs < 2^29): limbs < 2^30, value < 2^257
@@ -130,15 +146,30 @@ PBFTV_HD void fe_neg_lazy(fe& r, const fe& a) {
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = kP2Borrow[i] - a.v[i];
 }
 
+// A power of two the compiler cannot see: on the device, m * opaque(2^k) + t
+// becomes ONE v_mad_u64_u32 (multiplier in an SGPR) instead of a 64-bit
+// shift plus v_lshl_add_u64 (whose shift field only reaches 4).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t c) {
+  uint32_t r;
+  asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(c));
+  return r;
+}
+#else
+static inline uint32_t opaque_u32(uint32_t c) { return c; }
+#endif
+
 // Montgomery reduction of the 17 column accumulators (t[17] is scratch).
 PBFTV_HD void fe_mont_reduce_p(fe& r, uint64_t t[18]) {
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
+                 c24 = opaque_u32(1u << 24);
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     const uint32_t m = (uint32_t)t[i] & kMask29;
     t[i + 1] += t[i] >> 29;
-    t[i + 3] += (uint64_t)m << 9;
-    t[i + 6] += (uint64_t)m << 18;
-    t[i + 7] += (uint64_t)(m ^ kMask29) << 21;
-    t[i + 8] += (uint64_t)m << 24;
+    t[i + 3] += (uint64_t)m * c9;
+    t[i + 6] += (uint64_t)m * c18;
+    t[i + 7] += (uint64_t)(m ^ kMask29) * c21;
+    t[i + 8] += (uint64_t)m * c24;
   }
   PBFTV_UNROLL for (int j = 9; j < 16; ++j) {
     r.v[j - 9] = (uint32_t)t[j] & kMask29;

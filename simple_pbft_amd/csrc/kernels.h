@@ -13,9 +13,12 @@ size_t build_tables_scratch_bytes(uint32_t nkeys);
 hipError_t launch_build_tables(const uint32_t* keys_le, uint32_t nkeys, uint32_t* tables, uint32_t* valid,
                                void* scratch, hipStream_t st);
 size_t ecdsa_scratch_bytes(uint64_t n);
-// stage 1: scal (n * 64 B) + flag (n B) device scratch
+// stage 1: scal (n * 64 B) + flag (n B) + prefix (scalar_prefix_bytes(n)) device scratch
+int scalar_batch(uint64_t n);
+size_t scalar_prefix_bytes(uint64_t n);
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
-                                const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, hipStream_t st);
+                                const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, void* prefix,
+                                hipStream_t st);
 // stage 2: bitmap ceil(n/8) B
 hipError_t launch_ecdsa_comb(const void* scal, const uint8_t* flag, const uint8_t* sigs, const uint32_t* key_idx,
                              uint64_t n, const uint32_t* tables, uint8_t* bitmap, hipStream_t st);

@@ -38,7 +38,7 @@ struct jac {
 
 // dbl-2001-b, a = -3.  Input z != 0 assumed (caller tracks infinity); y == 0 impossible on P-256.
 PBFTV_HD void jac_double(jac& r, const jac& p) {
-  fe delta, gamma, beta, alpha, t1, t2, t3;
+  fe delta, gamma, beta, alpha, t1, t2, t3, b4;
   fe_sqr(delta, p.z);
   fe_sqr(gamma, p.y);
   fe_mul(beta, p.x, gamma);
@@ -47,26 +47,32 @@ PBFTV_HD void jac_double(jac& r, const jac& p) {
   fe_mul(t3, t1, t2);
   fe_mul_small(alpha, t3, 3);          // 3 (X - d)(X + d)
   fe_sqr(t1, alpha);
-  fe_mul_small(t2, beta, 4);           // 4 beta
-  fe_add(t3, t2, t2);                  // 8 beta (lazy)
+  fe_mul_small(t2, beta, 2);
+  fe_mul_small(b4, t2, 2);             // 4 beta
+  fe_add(t3, b4, b4);                  // 8 beta (lazy)
   fe r_x;
   fe_sub(r_x, t1, t3);
   fe_add(t1, p.y, p.z);
   fe_sqr(t3, t1);
   fe_sub(t3, t3, gamma);
   fe_sub(r.z, t3, delta);
-  fe_sub(t2, t2, r_x);                 // 4beta - X3
+  fe_sub(t2, b4, r_x);                 // 4beta - X3
   fe_mul(t1, alpha, t2);
   fe_sqr(t3, gamma);
-  fe_mul_small(t3, t3, 4);
+  fe_mul_small(t3, t3, 2);
+  fe_mul_small(t3, t3, 2);
   fe_add(t3, t3, t3);                  // 8 gamma^2 (lazy)
   fe_sub(r.y, t1, t3);
   r.x = r_x;
 }
 
 // Mixed addition acc += (x2, y2) (madd-2007-bl), acc.z != 0.
-// Returns 0 normal; 1 if the points are equal (caller must double); 2 if the
-// sum is the point at infinity.  On 1/2 the accumulator is left unchanged.
+// kCheck: returns 0 normal; 1 if the points are equal (caller must double);
+// 2 if the sum is the point at infinity (accumulator unchanged on 1/2).
+// !kCheck: no test; in both exceptional cases H == 0 and the result has
+// Z3 = 2 Z1 H == 0, which every later addition preserves -- so a single
+// Z == 0 test after a whole comb detects that some step was exceptional.
+template <bool kCheck = true>
 PBFTV_HD int jac_madd(jac& acc, const fe& x2, const fe& y2) {
   fe z1z1, u2, s2, h, hh, i4, j, rr, v, t, t2;
   fe_sqr(z1z1, acc.z);
@@ -75,10 +81,11 @@ PBFTV_HD int jac_madd(jac& acc, const fe& x2, const fe& y2) {
   fe_mul(s2, y2, t);
   fe_sub(h, u2, acc.x);
   fe_sub(t, s2, acc.y);
-  if (fe_is_zero(h)) return fe_is_zero(t) ? 1 : 2;
+  if (kCheck && fe_is_zero(h)) return fe_is_zero(t) ? 1 : 2;
   fe_add(rr, t, t);                    // r = 2 (S2 - Y1), lazy
   fe_sqr(hh, h);
-  fe_mul_small(i4, hh, 4);             // I = 4 HH
+  fe_mul_small(t, hh, 2);
+  fe_add(i4, t, t);                    // I = 4 HH (lazy)
   fe_mul(j, h, i4);                    // J = H * I
   fe_mul(v, acc.x, i4);                // V = X1 * I
   fe_sqr(t, rr);                       // r^2
@@ -150,15 +157,54 @@ PBFTV_HD void fe_pow(fe& r, const fe& a, const uint32_t e[8]) {
 
 PBFTV_HD void fe_inv(fe& r, const fe& a) { fe_pow(r, a, kPMinus2); }
 
-// s^-1 * R mod n for s in Montgomery form (Fermat, exponent n - 2) using a
-// 4-bit fixed window over odd/even powers computed on the fly.
-PBFTV_HD void fn_inv_mont(fe& r, const fe& sm) {
-  fe acc;
-  fe_set(acc, kOneN);
-  for (int i = 255; i >= 0; --i) {
-    fn_sqr(acc, acc);
-    if ((kNMinus2[i >> 5] >> (i & 31)) & 1u) fn_mul(acc, acc, sm);
+// n repeated Montgomery squarings mod n (a real loop: keeps code size small)
+PBFTV_HD void fn_sqr_n(fe& a, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 1
+#endif
+  for (int i = 0; i < n; ++i) fn_sqr(a, a);
+}
+
+// x^v for odd v in [1, 15] from the precomputed odd powers (v is a
+// compile-time constant once the step loop below is unrolled).
+PBFTV_HD const fe& fn_pick(int v, const fe& p1, const fe& p3, const fe& p5, const fe& p7, const fe& p9,
+                           const fe& p11, const fe& p13, const fe& p15) {
+  return v == 1 ? p1 : v == 3 ? p3 : v == 5 ? p5 : v == 7 ? p7 : v == 9 ? p9 : v == 11 ? p11 : v == 13 ? p13 : p15;
+}
+
+// s^-1 * R mod n for s = sm in Montgomery form: Fermat x^(n-2) by an addition
+// chain -- the top half FFFFFFFF00000000FFFFFFFFFFFFFFFF from x^(2^32-1)
+// blocks, the low half by a 4-bit sliding window (kInvNSteps, generated and
+// self-checked by tools/gen_p256_consts.py): 253 squarings + 39 multiplies.
+PBFTV_HD void fn_inv_mont(fe& r, const fe& x) {
+  fe x2, p3, p5, p7, p9, p11, p13, p15;
+  fn_sqr(x2, x);
+  fn_mul(p3, x2, x);
+  fn_mul(p5, p3, x2);
+  fn_mul(p7, p5, x2);
+  fn_mul(p9, p7, x2);
+  fn_mul(p11, p9, x2);
+  fn_mul(p13, p11, x2);
+  fn_mul(p15, p13, x2);      // x^(2^4 - 1)
+  fe t8 = p15, t16, t32, acc;
+  fn_sqr_n(t8, 4);
+  fn_mul(t8, t8, p15);       // x^(2^8 - 1)
+  t16 = t8;
+  fn_sqr_n(t16, 8);
+  fn_mul(t16, t16, t8);      // x^(2^16 - 1)
+  t32 = t16;
+  fn_sqr_n(t32, 16);
+  fn_mul(t32, t32, t16);     // x^(2^32 - 1)
+  acc = t32;
+  fn_sqr_n(acc, 64);
+  fn_mul(acc, acc, t32);
+  fn_sqr_n(acc, 32);
+  fn_mul(acc, acc, t32);     // x^FFFFFFFF00000000FFFFFFFFFFFFFFFF
+  PBFTV_UNROLL for (int i = 0; i < (int)(sizeof(kInvNSteps) / sizeof(kInvNSteps[0])); ++i) {
+    fn_sqr_n(acc, kInvNSteps[i][0]);
+    fn_mul(acc, acc, fn_pick(kInvNSteps[i][1], x, p3, p5, p7, p9, p11, p13, p15));
   }
+  fn_sqr_n(acc, kInvNTail);
   r = acc;
 }
 
@@ -216,8 +262,8 @@ PBFTV_HD void entry_to_fe(fe& x, fe& y, const uint32_t e[16]) {
 // acc = u * B using table tab (kWindows x kEntries x 16 words).  Returns false
 // if the result is the point at infinity (u == 0).  TableLoad is a functor
 // load(tab, window, idx, words[16]) so device code can use wide loads.
-template <class Load>
-PBFTV_HD bool comb_mult(jac& acc, const uint32_t u_w[8], Load load) {
+template <bool kCheck, class Load>
+PBFTV_HD bool comb_pass(jac& acc, const uint32_t u_w[8], Load load) {
   bool inf = true;
   int c = 0;
   for (int i = 0; i < kWindows; ++i) {
@@ -239,14 +285,23 @@ PBFTV_HD bool comb_mult(jac& acc, const uint32_t u_w[8], Load load) {
       inf = false;
       continue;
     }
-    const int st = jac_madd(acc, x, y);
-    if (st == 1) {
-      jac_double(acc, acc);
-    } else if (st == 2) {
-      inf = true;  // unreachable for a proper comb, kept for completeness
-    }
+    const int st = jac_madd<kCheck>(acc, x, y);
+    if (st == 1) jac_double(acc, acc);
+    else if (st == 2) inf = true;
   }
   return !inf;
+}
+
+// acc = u * B using table tab (kWindows x kEntries x 16 words).  Returns false
+// if the result is the point at infinity (u == 0).  Load is a functor
+// load(window, idx, words[16]).  Fast unchecked pass; if it ended with Z == 0
+// some step hit the doubling / inverse case (impossible for a proper comb,
+// DESIGN.md) and the comb is recomputed with complete additions.
+template <class Load>
+PBFTV_HD bool comb_mult(jac& acc, const uint32_t u_w[8], Load load) {
+  const bool ok = comb_pass<false>(acc, u_w, load);
+  if (ok && fe_is_zero(acc.z)) return comb_pass<true>(acc, u_w, load);
+  return ok;
 }
 
 // ---- final check --------------------------------------------------------------

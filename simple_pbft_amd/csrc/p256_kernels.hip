@@ -13,6 +13,8 @@
 // oracle is tested in tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 #include "p256_algo.h"
 
@@ -60,30 +62,100 @@ __global__ void __launch_bounds__(64) k_build_tables(const uint32_t* __restrict_
 
 // ---------------------------------------------------------------------------
 // stage 1: scalars.  scal[i] = {u1[8], u2[8]} (LE words); flag[i] = 1 if the
-// signature passes the range checks and names a valid registered key.
+// signature passes Go's range checks and names a valid registered key.
+//
+// Each lane owns K signatures i = lane + j*L (j < K, L = lanes in the grid, so
+// every load/store is coalesced across the wave) and inverts all K values of s
+// with ONE Fermat inversion (Montgomery's trick): prefix products
+// c_j = s_0 ... s_j go to a limb-major scratch, inv = c_{K-1}^-1, then walking
+// back w_j = inv * c_{j-1}, inv *= s_j.  Per signature that is 7 Montgomery
+// multiplies + 292/K for the inversion instead of 292 + 4.
+__device__ __forceinline__ bool sig_ok(const uint8_t* __restrict__ sigs, const uint32_t* __restrict__ key_idx,
+                                       const uint32_t* __restrict__ key_valid, uint32_t nkeys, uint64_t i,
+                                       uint32_t r[8], uint32_t s[8]) {
+  const uint32_t k = key_idx[i];
+  load_be256(sigs + 64 * i, r);
+  load_be256(sigs + 64 * i + 32, s);
+  if (!(k < nkeys && key_valid[k] != 0)) return false;
+  if (words_is_zero(r) || words_is_zero(s)) return false;
+  return words_lt(r, kN32) && words_lt(s, kN32);
+}
+
+template <int K>
 __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict__ hashes,
                                                        const uint8_t* __restrict__ sigs,
                                                        const uint32_t* __restrict__ key_idx, uint64_t n,
                                                        const uint32_t* __restrict__ key_valid, uint32_t nkeys,
-                                                       uint4* __restrict__ scal, uint8_t* __restrict__ flag) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = key_idx[i];
-  bool ok = k < nkeys && key_valid[k] != 0;
-  uint32_t e[8], r[8], s[8], u1[8], u2[8];
-  load_be256(hashes + 32 * i, e);
-  load_be256(sigs + 64 * i, r);
-  load_be256(sigs + 64 * i + 32, s);
-  if (ok) ok = ecdsa_scalars(e, r, s, u1, u2);
-  if (!ok) {
-    for (int j = 0; j < 8; ++j) { u1[j] = 0; u2[j] = 0; }
+                                                       uint4* __restrict__ scal, uint8_t* __restrict__ flag,
+                                                       uint32_t* __restrict__ prefix) {
+  const uint64_t L = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  fe r2n, acc;
+  fe_set(r2n, kR2N);
+  fe_set(acc, kOneN);
+  uint32_t okm = 0;
+  for (int j = 0; j < K; ++j) {
+    const uint64_t i = lane + (uint64_t)j * L;
+    uint32_t r[8], sw[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    bool ok = false;
+    if (i < n) {
+      uint32_t s[8];
+      ok = sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s);
+      if (ok) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
+    }
+    fe sv, sm;
+    fe_from_words(sv, sw);
+    fn_mul(sm, sv, r2n);
+    fn_mul(acc, acc, sm);
+    if (K > 1)
+      PBFTV_UNROLL for (int l = 0; l < 9; ++l) prefix[((uint64_t)j * 9 + l) * L + lane] = acc.v[l];
+    okm |= (ok ? 1u : 0u) << j;
   }
-  uint4* o = scal + 4 * i;
-  o[0] = make_uint4(u1[0], u1[1], u1[2], u1[3]);
-  o[1] = make_uint4(u1[4], u1[5], u1[6], u1[7]);
-  o[2] = make_uint4(u2[0], u2[1], u2[2], u2[3]);
-  o[3] = make_uint4(u2[4], u2[5], u2[6], u2[7]);
-  flag[i] = ok ? 1 : 0;
+  fe inv;
+  fn_inv_mont(inv, acc);
+  for (int j = K - 1; j >= 0; --j) {
+    const uint64_t i = lane + (uint64_t)j * L;
+    const bool ok = (okm >> j) & 1u;
+    uint32_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    if (ok) {
+      load_be256(sigs + 64 * i, r);
+      load_be256(sigs + 64 * i + 32, s);
+    }
+    fe w;
+    if (K > 1 && j > 0) {
+      fe pre;
+      PBFTV_UNROLL for (int l = 0; l < 9; ++l) pre.v[l] = prefix[((uint64_t)(j - 1) * 9 + l) * L + lane];
+      fn_mul(w, inv, pre);
+      fe sv, sm;
+      fe_from_words(sv, s);
+      fn_mul(sm, sv, r2n);
+      fn_mul(inv, inv, sm);
+    } else {
+      w = inv;
+    }
+    if (i < n) {
+      uint32_t u1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, u2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (ok) {
+        uint32_t e[8];
+        load_be256(hashes + 32 * i, e);
+        fe ev, rv, t;
+        fe_from_words(ev, e);
+        fe_from_words(rv, r);
+        fn_mul(t, ev, w);  // e * s^-1 (e < 2^256 < 2n: the Montgomery product is < 2n)
+        fn_canon(t, t);
+        fe_to_words(u1, t);
+        fn_mul(t, rv, w);
+        fn_canon(t, t);
+        fe_to_words(u2, t);
+      }
+      uint4* o = scal + 4 * i;
+      o[0] = make_uint4(u1[0], u1[1], u1[2], u1[3]);
+      o[1] = make_uint4(u1[4], u1[5], u1[6], u1[7]);
+      o[2] = make_uint4(u2[0], u2[1], u2[2], u2[3]);
+      o[3] = make_uint4(u2[4], u2[5], u2[6], u2[7]);
+      flag[i] = ok ? 1 : 0;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -109,7 +181,8 @@ __device__ __forceinline__ void load_entry(const uint4* __restrict__ tab, int wi
   e[0] = p[0]; e[1] = p[1]; e[2] = p[2]; e[3] = p[3];
 }
 
-__device__ bool comb_dev(jac& acc, const uint32_t u[8], const uint4* __restrict__ tab) {
+template <bool kCheck>
+__device__ bool comb_dev_pass(jac& acc, const uint32_t u[8], const uint4* __restrict__ tab) {
   digit_stream ds;
   PBFTV_UNROLL for (int j = 0; j < 8; ++j) ds.w[j] = u[j];
   ds.carry = 0;
@@ -140,11 +213,20 @@ __device__ bool comb_dev(jac& acc, const uint32_t u[8], const uint4* __restrict_
       inf = false;
       continue;
     }
-    const int st = jac_madd(acc, x, y);
-    if (st == 1) jac_double(acc, acc);
-    else if (st == 2) inf = true;
+    const int st = jac_madd<kCheck>(acc, x, y);
+    if (kCheck) {
+      if (st == 1) jac_double(acc, acc);
+      else if (st == 2) inf = true;
+    }
   }
   return !inf;
+}
+
+// unchecked fast pass; a Z == 0 result means some step was exceptional -> rerun checked
+__device__ bool comb_dev(jac& acc, const uint32_t u[8], const uint4* __restrict__ tab) {
+  const bool ok = comb_dev_pass<false>(acc, u, tab);
+  if (ok && fe_is_zero(acc.z)) return comb_dev_pass<true>(acc, u, tab);
+  return ok;
 }
 
 __global__ void __launch_bounds__(256) k_ecdsa_comb(const uint4* __restrict__ scal, const uint8_t* __restrict__ flag,
@@ -189,12 +271,47 @@ size_t build_tables_scratch_bytes(uint32_t nkeys) {
 
 size_t table_bytes_per_base() { return kTableBytes; }
 
+// signatures per lane in the scalar stage: enough lanes for ~2 waves per SIMD
+// (256 CUs x 4 SIMDs x 64 lanes x 2), the rest batched into the inversion.
+int scalar_batch(uint64_t n) {
+  if (const char* e = getenv("PBFTV_SCALAR_BATCH")) {
+    const int k = atoi(e);
+    if (k == 1 || k == 2 || k == 4 || k == 8 || k == 16) return k;
+  }
+  const uint64_t lanes = 256ull * 4 * 64 * 2;
+  int k = 1;
+  while (k < 16 && n >= (uint64_t)(2 * k) * lanes) k *= 2;
+  return k;
+}
+
+size_t scalar_prefix_bytes(uint64_t n) {
+  const int k = scalar_batch(n);
+  const uint64_t L = ((n + k - 1) / k + 255) / 256 * 256;
+  return (size_t)k * 9 * L * 4;
+}
+
+template <int K>
+static void launch_scalars_k(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
+                             const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, uint32_t* prefix,
+                             hipStream_t st) {
+  const uint64_t lanes = (n + K - 1) / K;
+  const uint64_t blocks = (lanes + 255) / 256;
+  hipLaunchKernelGGL(k_ecdsa_scalars<K>, dim3((uint32_t)blocks), dim3(256), 0, st, hashes, sigs, key_idx, n,
+                     key_valid, nkeys, reinterpret_cast<uint4*>(scal), flag, prefix);
+}
+
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
-                                const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, hipStream_t st) {
+                                const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, void* prefix,
+                                hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(k_ecdsa_scalars, dim3((uint32_t)blocks), dim3(256), 0, st, hashes, sigs, key_idx, n, key_valid,
-                     nkeys, reinterpret_cast<uint4*>(scal), flag);
+  uint32_t* pf = reinterpret_cast<uint32_t*>(prefix);
+  switch (scalar_batch(n)) {
+    case 1: launch_scalars_k<1>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
+    case 2: launch_scalars_k<2>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
+    case 4: launch_scalars_k<4>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
+    case 8: launch_scalars_k<8>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
+    default: launch_scalars_k<16>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
+  }
   return hipGetLastError();
 }
 

@@ -74,7 +74,7 @@ struct Device {
   uint32_t nkeys = 0;
   bool have_keys = false;
   // ecdsa scratch
-  DevBuf hashes, sigs, key_idx, scal, flag, bitmap;
+  DevBuf hashes, sigs, key_idx, scal, flag, prefix, bitmap;
   // sha scratch
   DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
   // kernel timing (events recorded around launches while ctx timing is on)
@@ -214,7 +214,8 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
-    for (DevBuf* b : {&d->tables, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag, &d->bitmap,
+    for (DevBuf* b : {&d->tables, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag, &d->prefix,
+                      &d->bitmap,
                       &d->data, &d->offsets, &d->lengths, &d->order, &d->order_scratch, &d->digests, &d->expected,
                       &d->shabits})
       b->release();
@@ -238,6 +239,7 @@ int pbftv_reserve(pbftv_ctx* ctx, uint64_t n) {
     HIP_TRY(hipSetDevice(d.id));
     HIP_TRY(d.scal.ensure(n * 64));
     HIP_TRY(d.flag.ensure(n));
+    HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
   }
   return PBFTV_OK;
 }
@@ -384,9 +386,10 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   if (!d.have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
   HIP_TRY(d.scal.ensure(n * 64));
   HIP_TRY(d.flag.ensure(n));
+  HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_SCALARS, st, [&] {
     return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, d.scal.p,
-                                       d.flag.as<uint8_t>(), st);
+                                       d.flag.as<uint8_t>(), d.prefix.p, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
     return pbftv::launch_ecdsa_comb(d.scal.p, d.flag.as<uint8_t>(), d_sigs, d_key_idx, n, d.tables.as<uint32_t>(),

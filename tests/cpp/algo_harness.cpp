@@ -104,6 +104,38 @@ void h_build_g_table(uint32_t* table) {
   }
 }
 
+// u * G via the comb, unchecked (0) or complete-addition (1) path; affine
+// canonical plain (non-Montgomery) x||y as LE words.  Returns 0 for infinity.
+int h_comb(const uint32_t* u, const uint32_t* tab, int checked, uint32_t* out_xy) {
+  jac A;
+  auto load = [&](int win, int idx, uint32_t* o) {
+    memcpy(o, tab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64);
+  };
+  bool ok = checked ? comb_pass<true>(A, u, load) : comb_mult(A, u, load);
+  if (!ok) return 0;
+  fe zi, one, x, y;
+  fe_inv(zi, A.z);
+  uint32_t w[16];
+  jac_to_affine_words(w, A, zi);
+  entry_to_fe(x, y, w);
+  fe_set(one, kOneP);
+  fe t;
+  fe_from_words(t, w);
+  // from Montgomery: multiply by 1 (plain)
+  fe plain1;
+  const uint32_t p1[9] = {1, 0, 0, 0, 0, 0, 0, 0, 0};
+  fe_set(plain1, p1);
+  fe_mul(x, x, plain1);
+  fe_mul(y, y, plain1);
+  fe_canon(x, x);
+  fe_canon(y, y);
+  fe_to_words(out_xy, x);
+  fe_to_words(out_xy + 8, y);
+  (void)one;
+  (void)t;
+  return 1;
+}
+
 // Full pipeline on one signature given prebuilt tables.
 int h_verify(const uint8_t* hash, const uint8_t* rs, const uint32_t* gtab, const uint32_t* qtab, int key_valid) {
   if (!key_valid) return 0;

@@ -169,6 +169,19 @@ def test_ecdsa_random_vs_oracle(ver, oracle_lib):
     assert want.sum() > n // 2
 
 
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
+def test_ecdsa_scalar_batch_sizes(ver, oracle_lib, ecdsa_fixtures, k, monkeypatch):
+    """The batched-inversion scalar kernel for every K (signatures per lane),
+    with valid / corrupted / out-of-range signatures mixed inside each batch."""
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    reps = 9
+    H, S, K, E = (np.tile(hashes, (reps, 1)), np.tile(sigs, (reps, 1)), np.tile(kidx, reps), np.tile(expect, reps))
+    monkeypatch.setenv("PBFTV_SCALAR_BATCH", str(k))
+    ver.register_keys(keys)
+    got = ver.verify_batch(H, S, K)
+    assert (got == E).all()
+
+
 def test_ecdsa_large_tiled_property(ver, oracle_lib):
     """262,144 signatures (tiles of an oracle-signed pool) with 1 % corrupted at
     known positions: the accept bitmap must be exactly the complement of the
