@@ -47,9 +47,21 @@ N_ORDER = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
 FE_MUL, FE_SQR, FN_MUL = 81, 45, 162
 MADD = 7 * FE_MUL + 4 * FE_SQR                     # madd-2007-bl
 JADD = 12 * FE_MUL + 4 * FE_SQR                    # add-2007-bl (final complete add)
-# windows 0..31 nonzero w.p. 255/256, window 32 w.p. ~1/2; first nonzero is a load
-ADDS_PER_COMB = 32 * 255 / 256 + 0.5 - 1
-MACS_COMB = 2 * ADDS_PER_COMB * MADD + JADD + (FE_SQR + 2 * FE_MUL)
+CHECK = FE_SQR + 2 * FE_MUL                         # X == r Z^2 test (+ rare r + n retry)
+
+
+def macs_comb(gbits: int, qbits: int) -> float:
+    """Joint comb (p256_kernels.hip k_ecdsa_comb): one mixed addition per nonzero
+    signed digit of u1 (G table) and u2 (key table), minus the first (a load).
+    Windows below 256 bits are nonzero w.p. 1 - 2^-W; the top (carry) window
+    w.p. ~1/2 when 256 % W == 0, else its 256 % W real bits make it nonzero."""
+    def nonzero(w):
+        full = 256 // w
+        top = 0.5 if 256 % w == 0 else 1.0
+        return full * (1 - 2.0 ** -w) + top
+    return (nonzero(gbits) + nonzero(qbits) - 1) * MADD + CHECK
+
+
 INV_N = 292                                         # fn_inv_mont addition chain (p256_algo.h)
 
 
@@ -230,9 +242,11 @@ def main():
         scal_avg = scal_ms / max(scal_cnt, 1) * 1e-3
         kb = scalar_batch(n)
         ms = macs_scalars(kb)
+        gb, qb, tb = ver.table_config()
+        mc = macs_comb(gb, qb)
         kern = {
-            "ecdsa_comb": {"avg_ms": comb_avg * 1e3, "macs_per_verify": MACS_COMB,
-                           "achieved_tmacs": n * MACS_COMB / comb_avg / 1e12},
+            "ecdsa_comb": {"avg_ms": comb_avg * 1e3, "macs_per_verify": mc, "window_bits": [gb, qb],
+                           "achieved_tmacs": n * mc / comb_avg / 1e12},
             "ecdsa_scalars": {"avg_ms": scal_avg * 1e3, "macs_per_verify": ms, "sigs_per_lane": kb,
                               "achieved_tmacs": n * ms / scal_avg / 1e12},
         }
@@ -247,6 +261,7 @@ def main():
                            "unit": "TMAC/s (v_mad_u64_u32 limb MACs)", "frac": ach * 1e12 / MAD_PEAK,
                            "traffic": traffic}
         out["kernels"] = kern
+        out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
         if not args.no_extras and ws == 1:
             p50_4, p99_4 = qc_latency(ver, 4, 3, 2000, 11)
             p50_100, p99_100 = qc_latency(ver, 100, 67, 1000, 12)

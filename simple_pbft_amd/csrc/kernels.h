@@ -7,11 +7,27 @@
 namespace pbftv {
 
 // ---- ECDSA-P256 (p256_kernels.hip) ----
-size_t table_bytes_per_base();
-size_t build_tables_scratch_bytes(uint32_t nkeys);
-// tables: (nkeys + 1) comb tables, base 0 = G.  keys_le: nkeys x {x[8], y[8]} LE words.
-hipError_t launch_build_tables(const uint32_t* keys_le, uint32_t nkeys, uint32_t* tables, uint32_t* valid,
-                               void* scratch, hipStream_t st);
+// Comb tables: W-bit signed windows, W in {8, 12, 16}; table_bytes(W) per base
+// (8: 264 KiB, 12: 2.75 MiB, 16: 34 MiB).
+size_t table_bytes(int w);
+struct TableScratch {
+  void* bases;
+  void* lbuf;
+  void* hbuf;
+  void* small_scratch;
+  void* entry_scratch;
+  uint64_t entry_lanes;
+};
+struct TableScratchSizes {
+  size_t bases, lbuf, hbuf, small_scratch, entry_scratch;
+  uint64_t entry_lanes;
+};
+TableScratchSizes table_scratch_sizes(int w, uint32_t nbases);
+// Build nb tables (G first when with_g) of width w into tables (nb * table_bytes(w));
+// keys_le: {x[8], y[8]} LE words per key, key0 = first key of this launch;
+// valid[key] written for every key built.
+hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g,
+                               uint32_t* valid, uint32_t* tables, TableScratch& sc, hipStream_t st);
 size_t ecdsa_scratch_bytes(uint64_t n);
 // stage 1: scal (n * 64 B) + flag (n B) + prefix (scalar_prefix_bytes(n)) device scratch
 int scalar_batch(uint64_t n);
@@ -19,9 +35,11 @@ size_t scalar_prefix_bytes(uint64_t n);
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                                 const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, void* prefix,
                                 hipStream_t st);
-// stage 2: bitmap ceil(n/8) B
-hipError_t launch_ecdsa_comb(const void* scal, const uint8_t* flag, const uint8_t* sigs, const uint32_t* key_idx,
-                             uint64_t n, const uint32_t* tables, uint8_t* bitmap, hipStream_t st);
+// stage 2: (wg, wq) in {(16,16), (16,12), (16,8), (8,8)}; qtabs = nkeys tables of width wq;
+// bitmap ceil(n/8) B
+hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* flag, const uint8_t* sigs,
+                             const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
+                             uint8_t* bitmap, hipStream_t st);
 
 // ---- SHA-256 (sha256_kernels.hip) ----
 // data must stay readable 4 bytes past every message end (device allocations are padded).

@@ -23,12 +23,27 @@
 
 namespace pbftv {
 
+// Comb table geometry for W-bit signed windows: digits d_i in
+// [-(2^(W-1) - 1), 2^(W-1)], u = sum d_i 2^(W i); entry (i, |d|-1) holds
+// |d| * 2^(W i) * B as affine (x, y), canonical Montgomery-form, 8+8 LE words.
+template <int W>
+struct CombGeom {
+  static_assert(W >= 8 && W <= 16, "window width");
+  static_assert(256 % W <= W - 2, "top window must absorb the recoding carry");
+  static constexpr int kW = W;
+  static constexpr int kWin = 256 / W + 1;             // 33 (W=8), 22 (W=12), 17 (W=16)
+  static constexpr int kEnt = 1 << (W - 1);
+  static constexpr uint64_t kWords = (uint64_t)kWin * kEnt * 16;
+  static constexpr uint64_t kBytes = kWords * 4;
+};
+
+// legacy names for the W = 8 geometry
 constexpr int kWinBits = 8;
-constexpr int kWindows = 33;          // 256/8 + 1 (signed recoding carry)
-constexpr int kEntries = 128;         // |d| in [1, 128]
-constexpr int kEntryWords = 16;       // x[8], y[8] canonical Montgomery-form words
-constexpr uint64_t kTableWords = (uint64_t)kWindows * kEntries * kEntryWords;  // per base point
-constexpr uint64_t kTableBytes = kTableWords * 4;                               // 270,336 B
+constexpr int kWindows = CombGeom<8>::kWin;
+constexpr int kEntries = CombGeom<8>::kEnt;
+constexpr int kEntryWords = 16;
+constexpr uint64_t kTableWords = CombGeom<8>::kWords;
+constexpr uint64_t kTableBytes = CombGeom<8>::kBytes;
 
 struct jac {
   fe x, y, z;
@@ -165,11 +180,21 @@ PBFTV_HD void fn_sqr_n(fe& a, int n) {
   for (int i = 0; i < n; ++i) fn_sqr(a, a);
 }
 
-// x^v for odd v in [1, 15] from the precomputed odd powers (v is a
-// compile-time constant once the step loop below is unrolled).
-PBFTV_HD const fe& fn_pick(int v, const fe& p1, const fe& p3, const fe& p5, const fe& p7, const fe& p9,
-                           const fe& p11, const fe& p13, const fe& p15) {
-  return v == 1 ? p1 : v == 3 ? p3 : v == 5 ? p5 : v == 7 ? p7 : v == 9 ? p9 : v == 11 ? p11 : v == 13 ? p13 : p15;
+// acc *= x^v for odd v in [1, 15] from the precomputed odd powers.  A switch
+// (wave-uniform branch) rather than a reference pick, so the powers stay in
+// registers instead of being spilled to addressable scratch.
+PBFTV_HD void fn_mul_pow(fe& acc, int v, const fe& p1, const fe& p3, const fe& p5, const fe& p7, const fe& p9,
+                         const fe& p11, const fe& p13, const fe& p15) {
+  switch (v) {
+    case 1: fn_mul(acc, acc, p1); break;
+    case 3: fn_mul(acc, acc, p3); break;
+    case 5: fn_mul(acc, acc, p5); break;
+    case 7: fn_mul(acc, acc, p7); break;
+    case 9: fn_mul(acc, acc, p9); break;
+    case 11: fn_mul(acc, acc, p11); break;
+    case 13: fn_mul(acc, acc, p13); break;
+    default: fn_mul(acc, acc, p15); break;
+  }
 }
 
 // s^-1 * R mod n for s = sm in Montgomery form: Fermat x^(n-2) by an addition
@@ -200,9 +225,9 @@ PBFTV_HD void fn_inv_mont(fe& r, const fe& x) {
   fn_mul(acc, acc, t32);
   fn_sqr_n(acc, 32);
   fn_mul(acc, acc, t32);     // x^FFFFFFFF00000000FFFFFFFFFFFFFFFF
-  PBFTV_UNROLL for (int i = 0; i < (int)(sizeof(kInvNSteps) / sizeof(kInvNSteps[0])); ++i) {
+  for (int i = 0; i < (int)(sizeof(kInvNSteps) / sizeof(kInvNSteps[0])); ++i) {
     fn_sqr_n(acc, kInvNSteps[i][0]);
-    fn_mul(acc, acc, fn_pick(kInvNSteps[i][1], x, p3, p5, p7, p9, p11, p13, p15));
+    fn_mul_pow(acc, kInvNSteps[i][1], x, p3, p5, p7, p9, p11, p13, p15);
   }
   fn_sqr_n(acc, kInvNTail);
   r = acc;
@@ -243,14 +268,24 @@ PBFTV_HD bool ecdsa_scalars(const uint32_t e_w[8], const uint32_t r_w[8], const 
   return true;
 }
 
-// ---- signed 8-bit digits ----------------------------------------------------
-// digit i of u (LE words), carry-in c (0/1); returns d in [-127, 128], updates c.
-PBFTV_HD int signed_digit(const uint32_t u_w[8], int i, int& c) {
-  int b = i < 32 ? (int)((u_w[i >> 2] >> (8 * (i & 3))) & 0xFFu) : 0;
-  int d = b + c;
-  c = d > 128 ? 1 : 0;
-  return d - (c << 8);
+// ---- signed W-bit digits --------------------------------------------------------
+// digit i of u (LE words), carry-in c (0/1); returns d in [-(2^(W-1)-1), 2^(W-1)], updates c.
+template <int W>
+PBFTV_HD int signed_digit_w(const uint32_t u_w[8], int i, int& c) {
+  const int bit = W * i;
+  uint32_t b = 0;
+  if (bit < 256) {
+    const int wi = bit >> 5, sh = bit & 31;
+    uint64_t two = u_w[wi];
+    if (wi + 1 < 8) two |= (uint64_t)u_w[wi + 1] << 32;
+    b = (uint32_t)(two >> sh) & ((1u << W) - 1u);
+  }
+  const int d = (int)b + c;
+  c = d > (1 << (W - 1)) ? 1 : 0;
+  return d - (c << W);
 }
+
+PBFTV_HD int signed_digit(const uint32_t u_w[8], int i, int& c) { return signed_digit_w<8>(u_w, i, c); }
 
 // unpack a table entry (16 words: x[8], y[8]) into field elements
 PBFTV_HD void entry_to_fe(fe& x, fe& y, const uint32_t e[16]) {
@@ -258,78 +293,95 @@ PBFTV_HD void entry_to_fe(fe& x, fe& y, const uint32_t e[16]) {
   fe_from_words(y, e + 8);
 }
 
-// ---- stage 2: comb ------------------------------------------------------------
-// acc = u * B using table tab (kWindows x kEntries x 16 words).  Returns false
-// if the result is the point at infinity (u == 0).  TableLoad is a functor
-// load(tab, window, idx, words[16]) so device code can use wide loads.
-template <bool kCheck, class Load>
-PBFTV_HD bool comb_pass(jac& acc, const uint32_t u_w[8], Load load) {
+// ---- stage 2: joint comb -------------------------------------------------------
+// R = u1*G + u2*Q accumulated in ONE Jacobian point: for every window i the G
+// entry of digit d1_i and the Q entry of digit d2_i are added (mixed
+// additions).  For honest inputs no step is exceptional; an adversarial
+// (r, s, e) can force a partial sum to meet the next table point (doubling)
+// or its negative (cancellation), and in both cases the unchecked addition
+// yields Z == 0, which later additions preserve.  So a single Z == 0 test at
+// the end decides whether to recompute the lane with complete additions
+// (kCheck), which handle doubling and the point at infinity exactly.
+
+// Add table entry (|d|-1) of window i with sign(d) to acc.
+template <bool kCheck>
+PBFTV_HD void comb_add_entry(jac& acc, bool& inf, int d, const uint32_t ew[16]) {
+  fe x, y;
+  entry_to_fe(x, y, ew);
+  if (d < 0) {
+    fe ny;
+    fe_neg_lazy(ny, y);
+    fe_norm(y, ny);
+  }
+  if (inf) {
+    acc.x = x;
+    acc.y = y;
+    fe_set(acc.z, kOneP);
+    inf = false;
+    return;
+  }
+  const int st = jac_madd<kCheck>(acc, x, y);
+  if (kCheck) {
+    if (st == 1) {
+      jac p;
+      p.x = x;
+      p.y = y;
+      fe_set(p.z, kOneP);
+      jac_double(acc, p);
+    } else if (st == 2) {
+      inf = true;
+    }
+  }
+}
+
+template <bool kCheck, int WG, int WQ, class LoadG, class LoadQ>
+PBFTV_HD bool comb2_pass(jac& acc, const uint32_t u1[8], const uint32_t u2[8], LoadG load_g, LoadQ load_q) {
+  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  constexpr int nW = nG > nQ ? nG : nQ;
   bool inf = true;
-  int c = 0;
-  for (int i = 0; i < kWindows; ++i) {
-    const int d = signed_digit(u_w, i, c);
-    if (d == 0) continue;
+  int c1 = 0, c2 = 0;
+  for (int i = 0; i < nW; ++i) {
     uint32_t ew[16];
-    load(i, (d < 0 ? -d : d) - 1, ew);
-    fe x, y;
-    entry_to_fe(x, y, ew);
-    if (d < 0) {
-      fe ny;
-      fe_neg_lazy(ny, y);
-      fe_norm(y, ny);
+    if (i < nG) {
+      const int d1 = signed_digit_w<WG>(u1, i, c1);
+      if (d1 != 0) {
+        load_g(i, (d1 < 0 ? -d1 : d1) - 1, ew);
+        comb_add_entry<kCheck>(acc, inf, d1, ew);
+      }
     }
-    if (inf) {
-      acc.x = x;
-      acc.y = y;
-      fe_set(acc.z, kOneP);
-      inf = false;
-      continue;
+    if (i < nQ) {
+      const int d2 = signed_digit_w<WQ>(u2, i, c2);
+      if (d2 != 0) {
+        load_q(i, (d2 < 0 ? -d2 : d2) - 1, ew);
+        comb_add_entry<kCheck>(acc, inf, d2, ew);
+      }
     }
-    const int st = jac_madd<kCheck>(acc, x, y);
-    if (st == 1) jac_double(acc, acc);
-    else if (st == 2) inf = true;
   }
   return !inf;
 }
 
-// acc = u * B using table tab (kWindows x kEntries x 16 words).  Returns false
-// if the result is the point at infinity (u == 0).  Load is a functor
-// load(window, idx, words[16]).  Fast unchecked pass; if it ended with Z == 0
-// some step hit the doubling / inverse case (impossible for a proper comb,
-// DESIGN.md) and the comb is recomputed with complete additions.
-template <class Load>
-PBFTV_HD bool comb_mult(jac& acc, const uint32_t u_w[8], Load load) {
-  const bool ok = comb_pass<false>(acc, u_w, load);
-  if (ok && fe_is_zero(acc.z)) return comb_pass<true>(acc, u_w, load);
+// u1*G + u2*Q; false if the result is the point at infinity.  load_*(window,
+// idx, words[16]) fetch table entries of the WG- / WQ-bit tables.
+template <int WG = 8, int WQ = 8, class LoadG, class LoadQ>
+PBFTV_HD bool comb2_mult(jac& acc, const uint32_t u1[8], const uint32_t u2[8], LoadG load_g, LoadQ load_q) {
+  const bool ok = comb2_pass<false, WG, WQ>(acc, u1, u2, load_g, load_q);
+  if (ok && fe_is_zero(acc.z)) return comb2_pass<true, WG, WQ>(acc, u1, u2, load_g, load_q);
   return ok;
 }
 
 // ---- final check --------------------------------------------------------------
-// R = A + B with A, B possibly infinite; accept iff R finite and R.x mod n == r.
-PBFTV_HD bool ecdsa_final(const jac& A, bool a_ok, const jac& B, bool b_ok, const uint32_t r_w[8]) {
-  jac R;
-  bool ok;
-  if (!a_ok && !b_ok) return false;
-  if (!a_ok) {
-    R = B; ok = true;
-  } else if (!b_ok) {
-    R = A; ok = true;
-  } else {
-    const int st = jac_add(R, A, B);
-    if (st == 1) { jac_double(R, A); ok = true; }
-    else ok = (st == 0);
-  }
-  if (!ok) return false;
-  // X == r * Z^2 (mod p), or X == (r + n) Z^2 when r + n < p
-  fe z2, rr, r2p, lhs, x;
+// Accept iff R is finite and R.x mod n == r:  X == r Z^2 (mod p), or
+// X == (r + n) Z^2 when r + n < p.  No field inversion.
+PBFTV_HD bool ecdsa_check(const jac& R, bool finite, const uint32_t r_w[8]) {
+  if (!finite) return false;
+  fe z2, rr, r2p, lhs;
   fe_sqr(z2, R.z);
   fe_from_words(rr, r_w);
   fe_set(r2p, kR2P);
   fe_mul(rr, rr, r2p);        // r in Montgomery form
   fe_mul(lhs, rr, z2);
   if (fe_equal(lhs, R.x)) return true;
-  // r + n < p  <=>  r < p - n
-  if (words_lt(r_w, kPMinusN32)) {
+  if (words_lt(r_w, kPMinusN32)) {  // r + n < p
     uint32_t rn[8];
     uint64_t cy = 0;
     for (int i = 0; i < 8; ++i) {
@@ -340,7 +392,6 @@ PBFTV_HD bool ecdsa_final(const jac& A, bool a_ok, const jac& B, bool b_ok, cons
     fe_from_words(rr, rn);
     fe_mul(rr, rr, r2p);
     fe_mul(lhs, rr, z2);
-    (void)x;
     if (fe_equal(lhs, R.x)) return true;
   }
   return false;
@@ -434,6 +485,126 @@ PBFTV_HD void build_window(uint32_t* out, int win, const fe& bx, const fe& by, S
       zinv = inv;
     }
     jac_to_affine_words(out + (uint64_t)e * kEntryWords, pt, zinv);
+  }
+}
+
+// ---- generic (W-bit) table construction, three parallel phases --------------
+// For base B and window i let B_i = 2^(W i) B, E = 2^(W-1) entries, CL =
+// min(E, 256).  Entry idx (multiple m = idx + 1 = hi*CL + lo + 1) is
+//     m * B_i = H_hi + L_lo,  L_lo = (lo + 1) B_i,  H_hi = hi * (CL B_i),
+// so every entry is ONE addition of two precomputed affine points (hi = 0:
+// a copy of L).  Phase 1 (lane per window) finds B_i, phase 2 (lane per
+// window) the L and H tables, phase 3 (lane per 64-entry chunk) the sums;
+// each phase normalises its points to affine with one inversion per lane
+// (Montgomery's batch trick).  Scratch is a flat array of field elements
+// reached through st(slot, fe) / ld(slot, fe): point j uses slots 3j..3j+2,
+// the running Z product slot 3*cnt + j.
+
+// Montgomery-trick batch conversion of cnt Jacobian points (in scratch) to
+// canonical affine words out[16 j ...].
+template <class StoreF, class LoadF>
+PBFTV_HD void batch_to_affine(uint32_t* out, int cnt, StoreF st, LoadF ld) {
+  fe pre, z;
+  ld(2, pre);
+  st(3 * cnt, pre);
+  for (int j = 1; j < cnt; ++j) {
+    ld(3 * j + 2, z);
+    fe_mul(pre, pre, z);
+    st(3 * cnt + j, pre);
+  }
+  fe inv;
+  fe_inv(inv, pre);
+  for (int j = cnt - 1; j >= 0; --j) {
+    jac pt;
+    ld(3 * j, pt.x);
+    ld(3 * j + 1, pt.y);
+    ld(3 * j + 2, pt.z);
+    fe zinv;
+    if (j > 0) {
+      fe prev;
+      ld(3 * cnt + j - 1, prev);
+      fe_mul(zinv, inv, prev);
+      fe_mul(inv, inv, pt.z);
+    } else {
+      zinv = inv;
+    }
+    jac_to_affine_words(out + (uint64_t)j * 16, pt, zinv);
+  }
+}
+
+// Phase 1: out = affine words of 2^(W win) * (bx, by).
+PBFTV_HD void window_base(uint32_t out[16], int shift_bits, const fe& bx, const fe& by) {
+  jac cur;
+  cur.x = bx;
+  cur.y = by;
+  fe_set(cur.z, kOneP);
+  for (int k = 0; k < shift_bits; ++k) jac_double(cur, cur);
+  fe zi;
+  fe_inv(zi, cur.z);
+  jac_to_affine_words(out, cur, zi);
+}
+
+// Phase 2 helper: out[16 (k-1)] = k * P for k = 1..cnt (P affine words).
+template <class StoreF, class LoadF>
+PBFTV_HD void multiples(uint32_t* out, int cnt, const uint32_t pw[16], StoreF st, LoadF ld) {
+  fe px, py;
+  entry_to_fe(px, py, pw);
+  jac cur;
+  cur.x = px;
+  cur.y = py;
+  fe_set(cur.z, kOneP);
+  for (int k = 0; k < cnt; ++k) {
+    if (k == 1) jac_double(cur, cur);
+    else if (k >= 2) jac_madd<false>(cur, px, py);  // (k+1) P with k+1 <= 2^15 << n: never exceptional
+    st(3 * k, cur.x);
+    st(3 * k + 1, cur.y);
+    st(3 * k + 2, cur.z);
+  }
+  batch_to_affine(out, cnt, st, ld);
+}
+
+// Phase 3: out[16 j] = H + L[j] for j < cnt (H affine words; has_h = false: copy L).
+// H = hi*CL*B_i and L[j] = (lo+1) B_i meet only for hi = 1, lo + 1 = CL (a doubling).
+template <class StoreF, class LoadF>
+PBFTV_HD void sums_chunk(uint32_t* out, int cnt, bool has_h, const uint32_t hw[16], const uint32_t* L, StoreF st,
+                         LoadF ld) {
+  if (!has_h) {
+    for (int j = 0; j < cnt * 16; ++j) out[j] = L[j];
+    return;
+  }
+  fe hx, hy;
+  entry_to_fe(hx, hy, hw);
+  for (int j = 0; j < cnt; ++j) {
+    fe lx, ly;
+    entry_to_fe(lx, ly, L + (uint64_t)j * 16);
+    jac cur;
+    cur.x = hx;
+    cur.y = hy;
+    fe_set(cur.z, kOneP);
+    if (jac_madd<true>(cur, lx, ly) == 1) jac_double(cur, cur);
+    st(3 * j, cur.x);
+    st(3 * j + 1, cur.y);
+    st(3 * j + 2, cur.z);
+  }
+  batch_to_affine(out, cnt, st, ld);
+}
+
+// Whole table of one base on the CPU harness (tests) -- the device runs the
+// same phases as separate kernels (p256_kernels.hip).
+template <int W, class StoreF, class LoadF>
+PBFTV_HD void build_table_serial(uint32_t* table, const fe& bx, const fe& by, uint32_t* lbuf, uint32_t* hbuf,
+                                 StoreF st, LoadF ld) {
+  using G = CombGeom<W>;
+  constexpr int CL = G::kEnt < 256 ? G::kEnt : 256;
+  constexpr int NH = G::kEnt / CL;
+  for (int win = 0; win < G::kWin; ++win) {
+    uint32_t bw[16];
+    window_base(bw, W * win, bx, by);
+    multiples(lbuf, CL, bw, st, ld);
+    if (NH > 1) multiples(hbuf, NH - 1, lbuf + (uint64_t)(CL - 1) * 16, st, ld);
+    uint32_t* tw = table + (uint64_t)win * G::kEnt * 16;
+    for (int hi = 0; hi < NH; ++hi)
+      sums_chunk(tw + (uint64_t)hi * CL * 16, CL, hi > 0, hbuf + (uint64_t)(hi > 0 ? hi - 1 : 0) * 16, lbuf, st, ld);
   }
 }
 

@@ -31,33 +31,157 @@ __device__ __forceinline__ void load_be256(const uint8_t* __restrict__ p, uint32
 }
 
 // ---------------------------------------------------------------------------
-// table construction: lane = base * kWindows + window.  base 0 = G, base b>0 = key b-1.
-__global__ void __launch_bounds__(64) k_build_tables(const uint32_t* __restrict__ keys_le, uint32_t nkeys,
-                                                     uint32_t* __restrict__ tables, uint32_t* __restrict__ valid,
-                                                     fe* __restrict__ scratch) {
-  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nbases = nkeys + 1;
-  if (lane >= nbases * kWindows) return;
-  const uint32_t base = lane / kWindows, win = lane % kWindows;
-  fe bx, by;
-  bool ok = true;
-  if (base == 0) {
+// Table construction (p256_algo.h, "generic (W-bit) table construction"):
+// three kernels over all bases of a registration.  Base b of a launch is G
+// when with_g && b == 0, else key key0 + b - with_g.
+template <int W>
+struct TabGeom {
+  using G = CombGeom<W>;
+  static constexpr int CL = G::kEnt < 256 ? G::kEnt : 256;  // L table: (lo+1) B_i, lo < CL
+  static constexpr int NH = G::kEnt / CL;                   // H table: hi (CL B_i), 1 <= hi < NH
+  static constexpr int PC = CL < 64 ? CL : 64;              // entries per phase-3 lane
+};
+
+__device__ __forceinline__ bool load_base(const uint32_t* __restrict__ keys_le, uint32_t key0, uint32_t b, int with_g,
+                                          fe& bx, fe& by) {
+  if (with_g && b == 0) {
     fe_set(bx, kGxMont);
     fe_set(by, kGyMont);
-  } else {
-    uint32_t xw[8], yw[8];
-    const uint32_t* k = keys_le + (uint64_t)(base - 1) * 16;
-    for (int i = 0; i < 8; ++i) { xw[i] = k[i]; yw[i] = k[8 + i]; }
-    ok = key_check(xw, yw, bx, by);
+    return true;
   }
-  uint32_t* out = tables + (uint64_t)base * kTableWords + (uint64_t)win * kEntries * kEntryWords;
-  if (win == 0 && base > 0) valid[base - 1] = ok ? 1u : 0u;
-  if (!ok) {
-    for (int i = 0; i < kEntries * kEntryWords; ++i) out[i] = 0;
-    return;
+  const uint32_t* k = keys_le + (uint64_t)(key0 + b - with_g) * 16;
+  uint32_t xw[8], yw[8];
+  for (int i = 0; i < 8; ++i) { xw[i] = k[i]; yw[i] = k[8 + i]; }
+  if (key_check(xw, yw, bx, by)) return true;
+  fe_set(bx, kGxMont);  // invalid key: build a harmless table (never used: valid[] = 0)
+  fe_set(by, kGyMont);
+  return false;
+}
+
+// phase 1: lane (b, win) -> bases[(b*nwin + win)*16] = 2^(W win) B affine; valid flags for keys
+template <int W>
+__global__ void __launch_bounds__(64) k_tab_bases(const uint32_t* __restrict__ keys_le, uint32_t key0, uint32_t nb,
+                                                  int with_g, uint32_t* __restrict__ valid,
+                                                  uint32_t* __restrict__ bases) {
+  constexpr int nwin = CombGeom<W>::kWin;
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nb * nwin) return;
+  const uint32_t b = lane / nwin, win = lane % nwin;
+  fe bx, by;
+  const bool ok = load_base(keys_le, key0, b, with_g, bx, by);
+  if (win == 0 && !(with_g && b == 0)) valid[key0 + b - with_g] = ok ? 1u : 0u;
+  window_base(bases + (uint64_t)lane * 16, W * (int)win, bx, by);
+}
+
+// phase 2: lane (b, win) -> L = (lo+1) B_i (CL points) and H = hi (CL B_i) (NH-1 points)
+template <int W>
+__global__ void __launch_bounds__(64) k_tab_small(const uint32_t* __restrict__ bases, uint32_t nb,
+                                                  uint32_t* __restrict__ lbuf, uint32_t* __restrict__ hbuf,
+                                                  fe* __restrict__ scratch) {
+  using T = TabGeom<W>;
+  constexpr int nwin = CombGeom<W>::kWin;
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nb * nwin) return;
+  fe* sc = scratch + (uint64_t)lane * 4 * T::CL;
+  auto st = [&](int slot, const fe& v) { sc[slot] = v; };
+  auto ld = [&](int slot, fe& v) { v = sc[slot]; };
+  uint32_t bw[16];
+  for (int i = 0; i < 16; ++i) bw[i] = bases[(uint64_t)lane * 16 + i];
+  uint32_t* L = lbuf + (uint64_t)lane * T::CL * 16;
+  multiples(L, T::CL, bw, st, ld);
+  if (T::NH > 1) {
+    uint32_t mw[16];
+    for (int i = 0; i < 16; ++i) mw[i] = L[(uint64_t)(T::CL - 1) * 16 + i];
+    multiples(hbuf + (uint64_t)lane * (T::NH - 1) * 16, T::NH - 1, mw, st, ld);
   }
-  fe* sc = scratch + (uint64_t)lane * kScratchSlots;
-  build_window(out, (int)win, bx, by, [&](int s, const fe& v) { sc[s] = v; }, [&](int s, fe& v) { v = sc[s]; });
+}
+
+// phase 3: lane (b, win, hi, part) -> PC entries idx = hi*CL + part*PC + j of base b's table
+template <int W>
+__global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__ lbuf,
+                                                    const uint32_t* __restrict__ hbuf, uint32_t nb,
+                                                    uint32_t* __restrict__ tables, fe* __restrict__ scratch) {
+  using T = TabGeom<W>;
+  using G = CombGeom<W>;
+  constexpr int parts = T::CL / T::PC;
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t per_base = (uint64_t)G::kWin * T::NH * parts;
+  if (lane >= nb * per_base) return;
+  const uint32_t b = (uint32_t)(lane / per_base);
+  uint32_t rem = (uint32_t)(lane % per_base);
+  const uint32_t win = rem / (T::NH * parts);
+  rem %= T::NH * parts;
+  const uint32_t hi = rem / parts, part = rem % parts;
+  const uint64_t bw = (uint64_t)b * G::kWin + win;  // (base, window) index into lbuf/hbuf
+  const uint32_t* L = lbuf + (bw * T::CL + (uint64_t)part * T::PC) * 16;
+  uint32_t hw[16] = {0};
+  if (hi > 0)
+    for (int i = 0; i < 16; ++i) hw[i] = hbuf[(bw * (T::NH - 1) + hi - 1) * 16 + i];
+  uint32_t* out = tables + (uint64_t)b * G::kWords + ((uint64_t)win * G::kEnt + (uint64_t)hi * T::CL +
+                                                      (uint64_t)part * T::PC) * 16;
+  fe* sc = scratch + (uint64_t)lane * 4 * T::PC;
+  sums_chunk(out, T::PC, hi > 0, hw, L, [&](int slot, const fe& v) { sc[slot] = v; },
+             [&](int slot, fe& v) { v = sc[slot]; });
+}
+
+template <int W>
+hipError_t build_tables_w(const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g, uint32_t* valid,
+                          uint32_t* tables, TableScratch& sc, hipStream_t st) {
+  using T = TabGeom<W>;
+  using G = CombGeom<W>;
+  if (nb == 0) return hipSuccess;
+  const uint32_t lanes12 = nb * G::kWin;
+  hipLaunchKernelGGL(k_tab_bases<W>, dim3((lanes12 + 63) / 64), dim3(64), 0, st, keys_le, key0, nb, with_g, valid,
+                     reinterpret_cast<uint32_t*>(sc.bases));
+  hipLaunchKernelGGL(k_tab_small<W>, dim3((lanes12 + 63) / 64), dim3(64), 0, st,
+                     reinterpret_cast<const uint32_t*>(sc.bases), nb, reinterpret_cast<uint32_t*>(sc.lbuf),
+                     reinterpret_cast<uint32_t*>(sc.hbuf), reinterpret_cast<fe*>(sc.small_scratch));
+  // phase 3 in groups of bases so its scratch stays within sc.entry_lanes lanes
+  constexpr uint64_t per_base = (uint64_t)G::kWin * T::NH * (T::CL / T::PC);
+  const uint32_t group = (uint32_t)(sc.entry_lanes / per_base > 0 ? sc.entry_lanes / per_base : 1);
+  for (uint32_t b0 = 0; b0 < nb; b0 += group) {
+    const uint32_t g = nb - b0 < group ? nb - b0 : group;
+    const uint64_t lanes3 = (uint64_t)g * per_base;
+    hipLaunchKernelGGL(k_tab_entries<W>, dim3((uint32_t)((lanes3 + 63) / 64)), dim3(64), 0, st,
+                       reinterpret_cast<const uint32_t*>(sc.lbuf) + (uint64_t)b0 * G::kWin * T::CL * 16,
+                       reinterpret_cast<const uint32_t*>(sc.hbuf) + (uint64_t)b0 * G::kWin * (T::NH > 1 ? T::NH - 1 : 0) * 16,
+                       g, tables + (uint64_t)b0 * G::kWords, reinterpret_cast<fe*>(sc.entry_scratch));
+  }
+  return hipGetLastError();
+}
+
+TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
+  TableScratchSizes z{};
+  auto fill = [&](auto geom) {
+    using G = decltype(geom);
+    using T = TabGeom<G::kW>;
+    z.bases = (size_t)nb * G::kWin * 64;
+    z.lbuf = (size_t)nb * G::kWin * T::CL * 64;
+    z.hbuf = (size_t)nb * G::kWin * (T::NH > 1 ? T::NH - 1 : 1) * 64;
+    z.small_scratch = (size_t)nb * G::kWin * 4 * T::CL * sizeof(fe);
+    const uint64_t per_base = (uint64_t)G::kWin * T::NH * (T::CL / T::PC);
+    const uint64_t lanes = per_base * nb < (uint64_t)(1 << 16) ? per_base * nb : (per_base > (1 << 16) ? per_base : (1 << 16));
+    z.entry_lanes = lanes;
+    z.entry_scratch = (size_t)lanes * 4 * T::PC * sizeof(fe);
+  };
+  if (w == 8) fill(CombGeom<8>());
+  else if (w == 12) fill(CombGeom<12>());
+  else fill(CombGeom<16>());
+  return z;
+}
+
+size_t table_bytes(int w) {
+  return w == 8 ? CombGeom<8>::kBytes : w == 12 ? CombGeom<12>::kBytes : CombGeom<16>::kBytes;
+}
+
+hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g,
+                               uint32_t* valid, uint32_t* tables, TableScratch& sc, hipStream_t st) {
+  switch (w) {
+    case 8: return build_tables_w<8>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    case 12: return build_tables_w<12>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    case 16: return build_tables_w<16>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -159,80 +283,84 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// stage 2: comb.  Signed 8-bit digits are peeled off a 256-bit register
-// shift (no runtime-indexed register arrays -> no scratch), and the table
-// entry for window i+1 is loaded while window i is being added.
+// stage 2: joint comb.  Signed W-bit digits are peeled off a 256-bit register
+// shift (no runtime-indexed register arrays -> no scratch), and the two table
+// entries of window i+1 are loaded while window i is being added.
+template <int W>
 struct digit_stream {
   uint32_t w[8];
   int carry;
   __device__ __forceinline__ int next() {
-    const int b = (int)(w[0] & 0xFFu);
-    PBFTV_UNROLL for (int j = 0; j < 7; ++j) w[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], 8);
-    w[7] >>= 8;
+    const int b = (int)(w[0] & ((1u << W) - 1u));
+    PBFTV_UNROLL for (int j = 0; j < 7; ++j) w[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], W);
+    w[7] >>= W;
     const int d = b + carry;
-    carry = d > 128 ? 1 : 0;
-    return d - (carry << 8);
+    carry = d > (1 << (W - 1)) ? 1 : 0;
+    return d - (carry << W);
   }
 };
 
+template <int W>
 __device__ __forceinline__ void load_entry(const uint4* __restrict__ tab, int win, int d, uint4 e[4]) {
   const int idx = (d < 0 ? -d : d) - 1;
-  const uint4* p = tab + ((uint64_t)win * kEntries + (idx < 0 ? 0 : idx)) * 4;
+  const uint4* p = tab + ((uint64_t)win * CombGeom<W>::kEnt + (idx < 0 ? 0 : idx)) * 4;
   e[0] = p[0]; e[1] = p[1]; e[2] = p[2]; e[3] = p[3];
 }
 
-template <bool kCheck>
-__device__ bool comb_dev_pass(jac& acc, const uint32_t u[8], const uint4* __restrict__ tab) {
-  digit_stream ds;
-  PBFTV_UNROLL for (int j = 0; j < 8; ++j) ds.w[j] = u[j];
-  ds.carry = 0;
-  int d = ds.next();
-  uint4 e[4];
-  load_entry(tab, 0, d, e);
+__device__ __forceinline__ void entry_words(const uint4 e[4], uint32_t ew[16]) {
+  PBFTV_UNROLL for (int q = 0; q < 4; ++q) {
+    ew[4 * q] = e[q].x; ew[4 * q + 1] = e[q].y; ew[4 * q + 2] = e[q].z; ew[4 * q + 3] = e[q].w;
+  }
+}
+
+template <bool kCheck, int WG, int WQ>
+__device__ bool comb2_dev_pass(jac& acc, const uint32_t u1[8], const uint32_t u2[8],
+                               const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
+  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  constexpr int nW = nG > nQ ? nG : nQ;
+  digit_stream<WG> s1;
+  digit_stream<WQ> s2;
+  PBFTV_UNROLL for (int j = 0; j < 8; ++j) { s1.w[j] = u1[j]; s2.w[j] = u2[j]; }
+  s1.carry = s2.carry = 0;
+  int d1 = s1.next(), d2 = s2.next();
+  uint4 eg[4], eq[4];
+  load_entry<WG>(gtab, 0, d1, eg);
+  load_entry<WQ>(qtab, 0, d2, eq);
   bool inf = true;
-  for (int i = 0; i < kWindows; ++i) {
-    const int dc = d;
-    uint32_t ew[16] = {e[0].x, e[0].y, e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w,
-                       e[2].x, e[2].y, e[2].z, e[2].w, e[3].x, e[3].y, e[3].z, e[3].w};
-    if (i + 1 < kWindows) {
-      d = ds.next();
-      load_entry(tab, i + 1, d, e);
+  for (int i = 0; i < nW; ++i) {
+    const int c1 = i < nG ? d1 : 0, c2 = i < nQ ? d2 : 0;
+    uint32_t wg[16], wq[16];
+    entry_words(eg, wg);
+    entry_words(eq, wq);
+    if (i + 1 < nG) {
+      d1 = s1.next();
+      load_entry<WG>(gtab, i + 1, d1, eg);
     }
-    if (dc == 0) continue;
-    fe x, y;
-    entry_to_fe(x, y, ew);
-    if (dc < 0) {
-      fe ny;
-      fe_neg_lazy(ny, y);
-      fe_norm(y, ny);
+    if (i + 1 < nQ) {
+      d2 = s2.next();
+      load_entry<WQ>(qtab, i + 1, d2, eq);
     }
-    if (inf) {
-      acc.x = x;
-      acc.y = y;
-      fe_set(acc.z, kOneP);
-      inf = false;
-      continue;
-    }
-    const int st = jac_madd<kCheck>(acc, x, y);
-    if (kCheck) {
-      if (st == 1) jac_double(acc, acc);
-      else if (st == 2) inf = true;
-    }
+    if (c1 != 0) comb_add_entry<kCheck>(acc, inf, c1, wg);
+    if (c2 != 0) comb_add_entry<kCheck>(acc, inf, c2, wq);
   }
   return !inf;
 }
 
-// unchecked fast pass; a Z == 0 result means some step was exceptional -> rerun checked
-__device__ bool comb_dev(jac& acc, const uint32_t u[8], const uint4* __restrict__ tab) {
-  const bool ok = comb_dev_pass<false>(acc, u, tab);
-  if (ok && fe_is_zero(acc.z)) return comb_dev_pass<true>(acc, u, tab);
-  return ok;
+// The complete-addition rerun is a real call so its registers do not
+// inflate the fast path's allocation (it runs only for exceptional lanes).
+template <int WG, int WQ>
+__device__ __noinline__ bool comb2_checked(jac& acc, const uint32_t u1[8], const uint32_t u2[8],
+                                           const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
+  return comb2_dev_pass<true, WG, WQ>(acc, u1, u2, gtab, qtab);
 }
 
-__global__ void __launch_bounds__(256) k_ecdsa_comb(const uint4* __restrict__ scal, const uint8_t* __restrict__ flag,
-                                                    const uint8_t* __restrict__ sigs,
-                                                    const uint32_t* __restrict__ key_idx, uint64_t n,
-                                                    const uint4* __restrict__ tables, uint8_t* __restrict__ bitmap) {
+template <int WG, int WQ>
+__global__ void __launch_bounds__(256, 2) k_ecdsa_comb(const uint4* __restrict__ scal, const uint8_t* __restrict__ flag,
+                                                       const uint8_t* __restrict__ sigs,
+                                                       const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                       const uint4* __restrict__ gtab,
+                                                       const uint4* __restrict__ qtabs,
+                                                       uint8_t* __restrict__ bitmap) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool ok = false;
   if (i < n && flag[i]) {
@@ -240,14 +368,13 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb(const uint4* __restrict__ sc
     const uint4 a = sp[0], b = sp[1], c = sp[2], dd = sp[3];
     const uint32_t u1[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     const uint32_t u2[8] = {c.x, c.y, c.z, c.w, dd.x, dd.y, dd.z, dd.w};
-    const uint4* gtab = tables;
-    const uint4* qtab = tables + (uint64_t)(key_idx[i] + 1) * (kTableWords / 4);
-    jac A, B;
-    const bool aok = comb_dev(A, u1, gtab);
-    const bool bok = comb_dev(B, u2, qtab);
+    const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
+    jac R;
+    bool fin = comb2_dev_pass<false, WG, WQ>(R, u1, u2, gtab, qtab);
+    if (fin && fe_is_zero(R.z)) fin = comb2_checked<WG, WQ>(R, u1, u2, gtab, qtab);  // exceptional step: redo
     uint32_t r[8];
     load_be256(sigs + 64 * i, r);
-    ok = ecdsa_final(A, aok, B, bok, r);
+    ok = ecdsa_check(R, fin, r);
   }
   // LSB-first bitmap: wave ballot, lanes 0..7 store one byte each
   const unsigned long long m = __ballot(ok);
@@ -255,21 +382,6 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb(const uint4* __restrict__ sc
   const uint64_t wave_base = i - lane;
   if (lane < 8 && wave_base + 8 * lane < n) bitmap[(wave_base >> 3) + lane] = (uint8_t)(m >> (8 * lane));
 }
-
-// ---------------------------------------------------------------------------
-hipError_t launch_build_tables(const uint32_t* keys_le, uint32_t nkeys, uint32_t* tables, uint32_t* valid,
-                               void* scratch, hipStream_t st) {
-  const uint32_t lanes = (nkeys + 1) * kWindows;
-  hipLaunchKernelGGL(k_build_tables, dim3((lanes + 63) / 64), dim3(64), 0, st, keys_le, nkeys, tables, valid,
-                     reinterpret_cast<fe*>(scratch));
-  return hipGetLastError();
-}
-
-size_t build_tables_scratch_bytes(uint32_t nkeys) {
-  return (size_t)(nkeys + 1) * kWindows * kScratchSlots * sizeof(fe);
-}
-
-size_t table_bytes_per_base() { return kTableBytes; }
 
 // signatures per lane in the scalar stage: enough lanes for ~2 waves per SIMD
 // (256 CUs x 4 SIMDs x 64 lanes x 2), the rest batched into the inversion.
@@ -315,12 +427,24 @@ hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, cons
   return hipGetLastError();
 }
 
-hipError_t launch_ecdsa_comb(const void* scal, const uint8_t* flag, const uint8_t* sigs, const uint32_t* key_idx,
-                             uint64_t n, const uint32_t* tables, uint8_t* bitmap, hipStream_t st) {
-  if (n == 0) return hipSuccess;
+template <int WG, int WQ>
+static void launch_comb_w(const void* scal, const uint8_t* flag, const uint8_t* sigs, const uint32_t* key_idx,
+                          uint64_t n, const uint32_t* gtab, const uint32_t* qtabs, uint8_t* bitmap, hipStream_t st) {
   const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(k_ecdsa_comb, dim3((uint32_t)blocks), dim3(256), 0, st, reinterpret_cast<const uint4*>(scal),
-                     flag, sigs, key_idx, n, reinterpret_cast<const uint4*>(tables), bitmap);
+  hipLaunchKernelGGL((k_ecdsa_comb<WG, WQ>), dim3((uint32_t)blocks), dim3(256), 0, st,
+                     reinterpret_cast<const uint4*>(scal), flag, sigs, key_idx, n,
+                     reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4*>(qtabs), bitmap);
+}
+
+hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* flag, const uint8_t* sigs,
+                             const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
+                             uint8_t* bitmap, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (wg == 16 && wq == 16) launch_comb_w<16, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 16 && wq == 12) launch_comb_w<16, 12>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 16 && wq == 8) launch_comb_w<16, 8>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 8 && wq == 8) launch_comb_w<8, 8>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -69,8 +70,9 @@ struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  // signature state
-  DevBuf tables, key_valid;
+  // signature state: comb table of G (width gbits) and of every registered key (width qbits)
+  DevBuf gtab, qtabs, key_valid;
+  int gbits = 0, qbits = 0;
   uint32_t nkeys = 0;
   bool have_keys = false;
   // ecdsa scratch
@@ -214,7 +216,7 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
-    for (DevBuf* b : {&d->tables, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag, &d->prefix,
+    for (DevBuf* b : {&d->gtab, &d->qtabs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag, &d->prefix,
                       &d->bitmap,
                       &d->data, &d->offsets, &d->lengths, &d->order, &d->order_scratch, &d->digests, &d->expected,
                       &d->shabits})
@@ -338,10 +340,51 @@ int pbftv_reset_kernel_times(pbftv_ctx* ctx) {
 }
 
 // ---------------------------------------------------------------- keys
+// Comb widths: G always 16-bit windows (34 MiB, shared); keys the widest of
+// 16 / 12 / 8 whose tables fit the budget (PBFTV_TABLE_BUDGET_MB, default
+// min(16 GiB, free HBM / 4)).  PBFTV_GBITS / PBFTV_QBITS override.
+static int env_bits(const char* name, int dflt) {
+  const char* e = getenv(name);
+  if (!e) return dflt;
+  const int v = atoi(e);
+  return (v == 8 || v == 12 || v == 16) ? v : dflt;
+}
+
+static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
+  *wg = env_bits("PBFTV_GBITS", 16);
+  size_t budget = std::min<size_t>(16ull << 30, free_bytes / 4);
+  if (const char* e = getenv("PBFTV_TABLE_BUDGET_MB")) budget = (size_t)atoll(e) << 20;
+  int q = 8;
+  for (int w : {16, 12}) {
+    if ((size_t)k * pbftv::table_bytes(w) <= budget) {
+      q = w;
+      break;
+    }
+  }
+  *wq = env_bits("PBFTV_QBITS", q);
+  if (*wg == 8) *wq = 8;  // instantiated combos: (16,16) (16,12) (16,8) (8,8)
+}
+
+static int build_tables(Device& d, int w, const uint32_t* d_keys, uint32_t nb, int with_g, uint32_t* valid,
+                        uint32_t* out) {
+  const pbftv::TableScratchSizes z = pbftv::table_scratch_sizes(w, nb);
+  DevBuf bases, lbuf, hbuf, ssc, esc;
+  HIP_TRY(bases.ensure(z.bases));
+  HIP_TRY(lbuf.ensure(z.lbuf));
+  HIP_TRY(hbuf.ensure(z.hbuf));
+  HIP_TRY(ssc.ensure(z.small_scratch));
+  HIP_TRY(esc.ensure(z.entry_scratch));
+  pbftv::TableScratch sc{bases.p, lbuf.p, hbuf.p, ssc.p, esc.p, z.entry_lanes};
+  HIP_TRY(pbftv::launch_build_tables(w, d_keys, 0, nb, with_g, valid, out, sc, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  for (DevBuf* b : {&bases, &lbuf, &hbuf, &ssc, &esc}) b->release();
+  return PBFTV_OK;
+}
+
 int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid) {
   if (!ctx || (k && !pub_xy)) return fail(PBFTV_EINVAL, "null argument");
   // big-endian X||Y -> little-endian 32-bit words
-  std::vector<uint32_t> le((size_t)k * 16);
+  std::vector<uint32_t> le((size_t)k * 16 + 16);
   for (uint32_t j = 0; j < k; ++j) {
     for (int c = 0; c < 2; ++c) {
       const uint8_t* b = pub_xy + 64ull * j + 32 * c;
@@ -358,25 +401,47 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
     d.have_keys = false;
-    const size_t tbytes = (size_t)(k + 1) * pbftv::table_bytes_per_base();
-    HIP_TRY(d.tables.ensure(tbytes));
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    int wg, wq;
+    choose_bits(k, free_b + d.qtabs.cap, &wg, &wq);
+    if (d.gbits != wg) {  // G table: once per context (and width)
+      HIP_TRY(d.gtab.ensure(pbftv::table_bytes(wg)));
+      DevBuf dummy;
+      HIP_TRY(dummy.ensure(64));
+      int rc = build_tables(d, wg, nullptr, 1, 1, dummy.as<uint32_t>(), d.gtab.as<uint32_t>());
+      dummy.release();
+      if (rc != PBFTV_OK) return rc;
+      d.gbits = wg;
+    }
+    HIP_TRY(d.qtabs.ensure((size_t)(k ? k : 1) * pbftv::table_bytes(wq)));
     HIP_TRY(d.key_valid.ensure((size_t)(k ? k : 1) * 4));
-    DevBuf keys, scratch;
-    HIP_TRY(keys.ensure(le.size() * 4 + 4));
-    if (k) HIP_TRY(hipMemcpyAsync(keys.p, le.data(), le.size() * 4, hipMemcpyHostToDevice, d.stream));
-    HIP_TRY(scratch.ensure(pbftv::build_tables_scratch_bytes(k)));
-    HIP_TRY(pbftv::launch_build_tables(keys.as<uint32_t>(), k, d.tables.as<uint32_t>(), d.key_valid.as<uint32_t>(),
-                                       scratch.p, d.stream));
-    if (first && k) HIP_TRY(hipMemcpyAsync(valid.data(), d.key_valid.p, (size_t)k * 4, hipMemcpyDeviceToHost, d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));
+    DevBuf keys;
+    HIP_TRY(keys.ensure(le.size() * 4));
+    HIP_TRY(hipMemcpyAsync(keys.p, le.data(), le.size() * 4, hipMemcpyHostToDevice, d.stream));
+    if (k) {
+      int rc = build_tables(d, wq, keys.as<uint32_t>(), k, 0, d.key_valid.as<uint32_t>(), d.qtabs.as<uint32_t>());
+      if (rc != PBFTV_OK) return rc;
+    }
+    if (first && k) HIP_TRY(hipMemcpy(valid.data(), d.key_valid.p, (size_t)k * 4, hipMemcpyDeviceToHost));
     keys.release();
-    scratch.release();
+    d.qbits = wq;
     d.nkeys = k;
     d.have_keys = true;
     first = false;
   }
   if (out_valid)
     for (uint32_t j = 0; j < k; ++j) out_valid[j] = valid[j] ? 1 : 0;
+  return PBFTV_OK;
+}
+
+int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uint64_t* out_table_bytes) {
+  if (!ctx || ctx->devs.empty()) return fail(PBFTV_EINVAL, "ctx is null");
+  const Device& d = *ctx->devs[0];
+  if (out_gbits) *out_gbits = d.gbits;
+  if (out_qbits) *out_qbits = d.qbits;
+  if (out_table_bytes)
+    *out_table_bytes = (d.gbits ? pbftv::table_bytes(d.gbits) : 0) + (d.qbits ? (uint64_t)d.nkeys * pbftv::table_bytes(d.qbits) : 0);
   return PBFTV_OK;
 }
 
@@ -392,8 +457,8 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
                                        d.flag.as<uint8_t>(), d.prefix.p, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
-    return pbftv::launch_ecdsa_comb(d.scal.p, d.flag.as<uint8_t>(), d_sigs, d_key_idx, n, d.tables.as<uint32_t>(),
-                                    d_bitmap, st);
+    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.scal.p, d.flag.as<uint8_t>(), d_sigs, d_key_idx, n,
+                                    d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(), d_bitmap, st);
   }));
   return PBFTV_OK;
 }

@@ -90,6 +90,8 @@ def lib() -> ctypes.CDLL:
         "pbftv_verify_msg_batch": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _vp, ctypes.c_uint64, _vp, _vp,
                                                   _vp, _vp, _vp, _vp]),
         "pbftv_register_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+        "pbftv_table_config": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                              ctypes.POINTER(ctypes.c_uint64)]),
         "pbftv_ecdsa_p256_verify_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
         "pbftv_ecdsa_p256_verify_batch_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint64, _vp,
                                                              _vp]),
@@ -348,6 +350,12 @@ class Verifier:
         valid = np.zeros(max(k, 1), np.uint8)
         _check(self._L.pbftv_register_keys(self._h, pub_xy.ctypes.data, k, valid.ctypes.data))
         return valid[:k].astype(bool)
+
+    def table_config(self):
+        """(G window bits, key window bits, table bytes per device)."""
+        g, q, b = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint64()
+        _check(self._L.pbftv_table_config(self._h, ctypes.byref(g), ctypes.byref(q), ctypes.byref(b)))
+        return g.value, q.value, b.value
 
     def verify_batch(self, hashes: np.ndarray, sig_rs: np.ndarray, key_idx: np.ndarray) -> np.ndarray:
         hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)

@@ -104,35 +104,87 @@ void h_build_g_table(uint32_t* table) {
   }
 }
 
-// u * G via the comb, unchecked (0) or complete-addition (1) path; affine
-// canonical plain (non-Montgomery) x||y as LE words.  Returns 0 for infinity.
+}  // extern "C"
+
+// Table of width W (8, 10, 12) via the generic three-phase builder;
+// base = pub (64 B BE) or G when pub is null.  Returns key validity.
+template <int W>
+static int build_w(const uint8_t* pub_xy, uint32_t* table) {
+  fe xm, ym;
+  if (pub_xy) {
+    uint32_t xw[8], yw[8];
+    be32_to_le_words(pub_xy, xw);
+    be32_to_le_words(pub_xy + 32, yw);
+    if (!key_check(xw, yw, xm, ym)) return 0;
+  } else {
+    fe_set(xm, kGxMont);
+    fe_set(ym, kGyMont);
+  }
+  std::vector<fe> scratch(4 * 256);
+  std::vector<uint32_t> lbuf(256 * 16), hbuf(256 * 16);
+  build_table_serial<W>(table, xm, ym, lbuf.data(), hbuf.data(), [&](int slot, const fe& v) { scratch[slot] = v; },
+                        [&](int slot, fe& v) { v = scratch[slot]; });
+  return 1;
+}
+
+extern "C" {
+
+int h_build_table_w(const uint8_t* pub_xy, int w, uint32_t* table) {
+  switch (w) {
+    case 8: return build_w<8>(pub_xy, table);
+    case 10: return build_w<10>(pub_xy, table);
+    case 12: return build_w<12>(pub_xy, table);
+    default: return -1;
+  }
+}
+
+// Full pipeline with (WG, WQ) = (w, w) tables built by h_build_table_w.
+int h_verify_w(int w, const uint8_t* hash, const uint8_t* rs, const uint32_t* gtab, const uint32_t* qtab, int key_valid) {
+  if (!key_valid) return 0;
+  uint32_t e[8], r[8], s[8], u1[8], u2[8];
+  be32_to_le_words(hash, e);
+  be32_to_le_words(rs, r);
+  be32_to_le_words(rs + 32, s);
+  if (!ecdsa_scalars(e, r, s, u1, u2)) return 0;
+  jac R;
+  bool fin = false;
+  auto run = [&](auto geom) {
+    constexpr int W = decltype(geom)::kW;
+    auto lg = [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + ((uint64_t)win * CombGeom<W>::kEnt + idx) * 16, 64); };
+    auto lq = [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + ((uint64_t)win * CombGeom<W>::kEnt + idx) * 16, 64); };
+    fin = comb2_mult<W, W>(R, u1, u2, lg, lq);
+  };
+  if (w == 8) run(CombGeom<8>());
+  else if (w == 10) run(CombGeom<10>());
+  else if (w == 12) run(CombGeom<12>());
+  else return -1;
+  return ecdsa_check(R, fin, r) ? 1 : 0;
+}
+
+// u * G via the joint comb (u2 = 0), unchecked (0) or complete-addition (1)
+// path; affine canonical plain (non-Montgomery) x||y as LE words.  Returns 0
+// for the point at infinity.
 int h_comb(const uint32_t* u, const uint32_t* tab, int checked, uint32_t* out_xy) {
   jac A;
+  const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto load = [&](int win, int idx, uint32_t* o) {
     memcpy(o, tab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64);
   };
-  bool ok = checked ? comb_pass<true>(A, u, load) : comb_mult(A, u, load);
+  bool ok = checked ? comb2_pass<true, 8, 8>(A, u, zero, load, load) : comb2_mult(A, u, zero, load, load);
   if (!ok) return 0;
-  fe zi, one, x, y;
+  fe zi, x, y, plain1;
   fe_inv(zi, A.z);
   uint32_t w[16];
   jac_to_affine_words(w, A, zi);
   entry_to_fe(x, y, w);
-  fe_set(one, kOneP);
-  fe t;
-  fe_from_words(t, w);
-  // from Montgomery: multiply by 1 (plain)
-  fe plain1;
   const uint32_t p1[9] = {1, 0, 0, 0, 0, 0, 0, 0, 0};
   fe_set(plain1, p1);
-  fe_mul(x, x, plain1);
+  fe_mul(x, x, plain1);  // out of Montgomery form
   fe_mul(y, y, plain1);
   fe_canon(x, x);
   fe_canon(y, y);
   fe_to_words(out_xy, x);
   fe_to_words(out_xy + 8, y);
-  (void)one;
-  (void)t;
   return 1;
 }
 
@@ -144,14 +196,11 @@ int h_verify(const uint8_t* hash, const uint8_t* rs, const uint32_t* gtab, const
   be32_to_le_words(rs, r);
   be32_to_le_words(rs + 32, s);
   if (!ecdsa_scalars(e, r, s, u1, u2)) return 0;
-  jac A, B;
-  bool aok = comb_mult(A, u1, [&](int win, int idx, uint32_t* out) {
-    memcpy(out, gtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64);
-  });
-  bool bok = comb_mult(B, u2, [&](int win, int idx, uint32_t* out) {
-    memcpy(out, qtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64);
-  });
-  return ecdsa_final(A, aok, B, bok, r) ? 1 : 0;
+  jac R;
+  const bool fin = comb2_mult(
+      R, u1, u2, [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64); },
+      [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64); });
+  return ecdsa_check(R, fin, r) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -169,6 +169,28 @@ def test_ecdsa_random_vs_oracle(ver, oracle_lib):
     assert want.sum() > n // 2
 
 
+@pytest.mark.parametrize("gq", [(16, 16), (16, 12), (16, 8), (8, 8)])
+def test_ecdsa_every_table_width(oracle_lib, ecdsa_fixtures, gq, monkeypatch):
+    """Golden vectors + random corruptions vs the oracle for every comb geometry."""
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_GBITS", str(gq[0]))
+    monkeypatch.setenv("PBFTV_QBITS", str(gq[1]))
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    with Verifier() as v:
+        assert v.register_keys(keys).tolist() == [k["valid"] for k in ecdsa_fixtures["keys"]]
+        assert v.table_config()[:2] == gq
+        assert (v.verify_batch(hashes, sigs, kidx) == expect).all()
+        pk, h, sg, ki = oracle_sign_pool(oracle_lib, n_keys=5, per_key=50, seed=gq[0] * 100 + gq[1])
+        sg[::3, 7] ^= 0x20
+        v.register_keys(pk)
+        got = v.verify_batch(h, sg, ki)
+        n = len(ki)
+        bm = np.zeros((n + 7) // 8, np.uint8)
+        oracle_lib.oracle_ecdsa_p256_verify_batch(h.ctypes.data, sg.ctypes.data, ki.ctypes.data, n, pk.ctypes.data,
+                                                  len(pk), bm.ctypes.data, 8)
+        assert (got == np.unpackbits(bm, bitorder="little")[:n].astype(bool)).all()
+
+
 @pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
 def test_ecdsa_scalar_batch_sizes(ver, oracle_lib, ecdsa_fixtures, k, monkeypatch):
     """The batched-inversion scalar kernel for every K (signatures per lane),
