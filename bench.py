@@ -191,7 +191,10 @@ def main():
 
     ws, rank, local = dist_env()
     d = Dist(ws)
-    ver = Verifier(device_mask=1 << local)
+    # one GPU per rank; PBFTV_BENCH_SHARE_DEVICE=1 puts every rank on device 0
+    # (only to rehearse the N > 1 flow on a 1-GPU box -- not a scaling number)
+    share = os.environ.get("PBFTV_BENCH_SHARE_DEVICE") == "1"
+    ver = Verifier(device_mask=1 if share else 1 << local)
     n = args.n
     pub, H, S, K, ok = synth.config4(n, n_keys=args.keys, seed=0x50424654 + rank)
     valid = ver.register_keys(pub)
