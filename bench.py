@@ -179,6 +179,118 @@ def openssl_standin(pub, H, S, K, sample: int):
             "note": "OpenSSL 3 ECDSA_do_verify via ctypes incl. key/sig object setup per call"}
 
 
+# ---------------------------------------------------------------- other BASELINE configs
+def _timed(ver, fn, reps):
+    """Best-of wall time of fn() (each call synchronises the device)."""
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ver.sync(0)
+        ts.append(time.perf_counter() - t0)
+    return min(ts), float(np.median(ts))
+
+
+def run_config1(ver, n_req=1000):
+    """configs[0]: the reference 4-node pattern for 1k requests, end to end from
+    host buffers: request digests once, vote/reply preimage digests, every
+    prepare/commit/reply signature check (25 per request), verifyMsg on every vote."""
+    pub, reqs, votes, vsig, replies, rsig, checks = synth.config1_cluster(n_req)
+    ver.register_keys(pub)
+    node_of = {nid: j for j, nid in enumerate(synth.NODES)}
+    vk = np.array([node_of[v[3]] for v in votes], np.uint32)
+    rk = np.array([node_of[r[3]] for r in replies], np.uint32)
+    vi = np.array([c[1] for c in checks if c[0] == "vote"], np.int64)
+    ri = np.array([c[1] for c in checks if c[0] == "reply"], np.int64)
+    state = {}
+    seq_to_r = {reqs[r][3]: r for r in range(n_req)}
+    groups = {}
+    for j in vi:
+        groups.setdefault(seq_to_r[votes[j][1]], []).append(votes[j])
+
+    def flow():
+        from simple_pbft_amd.pbftv import verify_msg_batch
+        req_d = ver.digest_request_batch(reqs)                  # digest(request), once per request
+        vd = ver.digest_vote_batch(votes)                       # signed preimages
+        rd = ver.digest_reply_batch(replies)
+        H = np.concatenate([vd[vi], rd[ri]])
+        S = np.concatenate([vsig[vi], rsig[ri]])
+        K = np.concatenate([vk[vi], rk[ri]])
+        ok_sig = ver.verify_batch(H, S, K)
+        ok_msg = True                                           # State.verifyMsg on every received vote
+        for r, vv in groups.items():
+            res = verify_msg_batch(synth.VIEW, -1, req_d[r].tobytes(), [v[0] for v in vv], [v[1] for v in vv],
+                                   [v[2] for v in vv])
+            ok_msg = ok_msg and bool(res.all())
+        state["ok"] = bool(ok_sig.all()) and ok_msg
+
+    best, med = _timed(ver, flow, 5)
+    n_sig = len(vi) + len(ri)
+    return {"workload": f"config1: 4-node pattern, {n_req} requests, {n_sig} signature checks, "
+                        f"{len(reqs) + len(votes) + len(replies)} digests, end-to-end from host buffers",
+            "verifies_per_s": n_sig / best, "ms": best * 1e3, "ms_median": med * 1e3, "check": state.get("ok")}
+
+
+def run_certs(ver, n_keys, per_cert, n_certs, pool_certs, label):
+    pub, H, S, K = synth.certs(n_keys, per_cert, pool_certs, seed=per_cert * 7 + n_keys)
+    reps = -(-n_certs // pool_certs)
+    H, S, K = (np.tile(H, (reps, 1))[:n_certs * per_cert], np.tile(S, (reps, 1))[:n_certs * per_cert],
+               np.tile(K, reps)[:n_certs * per_cert])
+    ver.register_keys(pub)
+    n = len(K)
+    dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
+    db = ver.alloc(0, (n + 7) // 8)
+    best, med = _timed(ver, lambda: ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr), 10)
+    bits = np.unpackbits(db.to_host(), bitorder="little")[:n].reshape(n_certs, per_cert)
+    quorum_ok = bool((bits.sum(1) >= per_cert).all())
+    for b in (dh, ds, dk, db):
+        b.free()
+    return {"workload": label, "verifies_per_s": n / best, "ms": best * 1e3, "ms_median": med * 1e3,
+            "certs": n_certs, "check": quorum_ok}
+
+
+def run_config5(ver, n=1_000_000, steps=5):
+    """configs[4]: SHA-256 over 1M messages of 256 B..4 KiB (digest kernel alone)."""
+    import hashlib
+    data, off, ln = synth.sha_config5(n)
+    dd = ver.to_device(0, data, pad=64)
+    do, dl = ver.to_device(0, off), ver.to_device(0, ln)
+    dord, dg = ver.alloc(0, 4 * n), ver.alloc(0, 32 * n)
+    ver.sha256_order_dev(0, dl.ptr, n, dord.ptr)
+    ver.sync(0)
+    ver.set_kernel_timing(True)
+    ver.reset_kernel_times()
+    best, med = _timed(ver, lambda: ver.sha256_batch_dev(0, dd.ptr, do.ptr, dl.ptr, dord.ptr, n, dg.ptr), steps)
+    k_ms, k_cnt = ver.kernel_time_ms(0, 2)
+    ver.set_kernel_timing(False)
+    dig = dg.to_host().reshape(n, 32)
+    rng = np.random.default_rng(1)
+    ok = all(dig[i].tobytes() == hashlib.sha256(data[off[i]:off[i] + ln[i]].tobytes()).digest()
+             for i in rng.integers(0, n, 2000))
+    total = int(ln.sum())
+    blocks = int(((ln.astype(np.int64) + 8) // 64 + 1).sum())
+    kavg = k_ms / max(k_cnt, 1) * 1e-3
+    for b in (dd, do, dl, dord, dg):
+        b.free()
+    ops = blocks * SHA_OPS_PER_BLOCK
+    return {"workload": f"config5: SHA-256 of {n} messages, {lo_hi(ln)} B, {total / 1e9:.2f} GB, {blocks} blocks",
+            "digests_per_s": n / best, "GB_per_s": total / best / 1e9, "ms": best * 1e3, "kernel_ms": kavg * 1e3,
+            "roofline": {"bound": "valu", "achieved": ops / kavg / 1e12, "peak": VALU_PEAK / 1e12,
+                         "unit": "T VALU ops/s (1528 per 64-B block, SURVEY §8(d))",
+                         "frac": ops / kavg / VALU_PEAK, "hbm_GB_per_s": (total + 32 * n) / kavg / 1e9,
+                         "hbm_frac": (total + 32 * n) / kavg / 8e12},
+            "check": ok}
+
+
+def lo_hi(ln):
+    return f"{int(ln.min())}-{int(ln.max())}"
+
+
+SHA_OPS_PER_BLOCK = 1528
+VALU_PEAK = 256 * 4 * 32 * 2.4e9   # full-rate 32-bit VALU: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -281,6 +393,14 @@ def main():
             ost = openssl_standin(pub, H, S, K, sample=4000)
             if ost is not None:
                 out["cpu_openssl_standin"] = ost
+            out["other_configs"] = {
+                "config1": run_config1(ver),
+                "config2": run_certs(ver, 4, 6, 10000, 2000,
+                                     "config2: n=4, 10k requests x (3 prepare + 3 commit) sigs = 60k in one launch"),
+                "config3": run_certs(ver, 100, 67, 10000, 500,
+                                     "config3: n=100 committee, 10k certificates x 67 sigs = 670k on one GPU"),
+                "config5": run_config5(ver),
+            }
         print(json.dumps(out), flush=True)
     for b in (dh, ds, dk, db):
         b.free()

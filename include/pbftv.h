@@ -139,6 +139,19 @@ int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timest
                                const uint64_t* operation_off, const uint32_t* operation_len,
                                const int64_t* sequence_ids, uint8_t* out_digests);
 
+/* digest(*VoteMsg) / digest(*ReplyMsg) for n messages (the signed preimages of
+ * prepare/commit votes and replies): Go-JSON built on the host, one GPU SHA-256
+ * batch.  Byte strings are concatenated with per-item offsets/lengths. */
+int pbftv_digest_vote_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                            const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                            const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                            const int64_t* msg_types, uint8_t* out_digests);
+int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* timestamps,
+                             const uint8_t* client_ids, const uint64_t* client_id_off, const uint32_t* client_id_len,
+                             const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                             const uint8_t* results, const uint64_t* result_off, const uint32_t* result_len,
+                             uint8_t* out_digests);
+
 /* State.verifyMsg (pbft_impl.go:176-202) over n votes against one state:
  * bit i = view_ids[i] == state_view_id
  *         && (state_last_seq == -1 || state_last_seq < sequence_ids[i])

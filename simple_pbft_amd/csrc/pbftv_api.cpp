@@ -649,6 +649,56 @@ int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timest
   return pbftv_sha256_batch(ctx, buf.data(), off.data(), len.data(), n, out_digests);
 }
 
+static int hash_preimages(pbftv_ctx* ctx, const std::vector<uint8_t>& buf, const std::vector<uint64_t>& off,
+                          uint64_t n, uint8_t* out_digests) {
+  std::vector<uint32_t> len(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t l = (i + 1 < n ? off[i + 1] : buf.size()) - off[i];
+    if (l > 0xFFFFFFFFull) return fail(PBFTV_EINVAL, "preimage longer than 4 GiB");
+    len[i] = (uint32_t)l;
+  }
+  return pbftv_sha256_batch(ctx, buf.data(), off.data(), len.data(), n, out_digests);
+}
+
+int pbftv_digest_vote_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                            const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                            const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                            const int64_t* msg_types, uint8_t* out_digests) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!view_ids || !sequence_ids || !digest_off || !digest_len || !node_id_off || !node_id_len || !msg_types ||
+            !out_digests))
+    return fail(PBFTV_EINVAL, "null buffer");
+  std::vector<uint8_t> buf;
+  std::vector<uint64_t> off(n);
+  buf.reserve(n * 176);
+  for (uint64_t i = 0; i < n; ++i) {
+    off[i] = buf.size();
+    pbftv::gojson::append_vote(buf, view_ids[i], sequence_ids[i], digests + digest_off[i], digest_len[i],
+                               node_ids + node_id_off[i], node_id_len[i], msg_types[i]);
+  }
+  return hash_preimages(ctx, buf, off, n, out_digests);
+}
+
+int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* timestamps,
+                             const uint8_t* client_ids, const uint64_t* client_id_off, const uint32_t* client_id_len,
+                             const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                             const uint8_t* results, const uint64_t* result_off, const uint32_t* result_len,
+                             uint8_t* out_digests) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!view_ids || !timestamps || !client_id_off || !client_id_len || !node_id_off || !node_id_len ||
+            !result_off || !result_len || !out_digests))
+    return fail(PBFTV_EINVAL, "null buffer");
+  std::vector<uint8_t> buf;
+  std::vector<uint64_t> off(n);
+  buf.reserve(n * 120);
+  for (uint64_t i = 0; i < n; ++i) {
+    off[i] = buf.size();
+    pbftv::gojson::append_reply(buf, view_ids[i], timestamps[i], client_ids + client_id_off[i], client_id_len[i],
+                                node_ids + node_id_off[i], node_id_len[i], results + result_off[i], result_len[i]);
+  }
+  return hash_preimages(ctx, buf, off, n, out_digests);
+}
+
 int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const uint8_t req_digest[32], uint64_t n,
                            const int64_t* view_ids, const int64_t* sequence_ids, const char* digest_got,
                            const uint64_t* digest_got_off, const uint32_t* digest_got_len, uint8_t* out_bitmap) {

@@ -87,6 +87,8 @@ def lib() -> ctypes.CDLL:
                                                       ctypes.c_int64, _vp, ctypes.c_uint64]),
         "pbftv_digest_request_batch": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                                       _vp]),
+        "pbftv_digest_vote_batch": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 10),
+        "pbftv_digest_reply_batch": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 12),
         "pbftv_verify_msg_batch": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _vp, ctypes.c_uint64, _vp, _vp,
                                                   _vp, _vp, _vp, _vp]),
         "pbftv_register_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
@@ -341,6 +343,35 @@ class Verifier:
                                                   cid_off.ctypes.data, cid_len.ctypes.data, op_blob.ctypes.data,
                                                   op_off.ctypes.data, op_len.ctypes.data, seq.ctypes.data,
                                                   out.ctypes.data))
+        return out[:n]
+
+    def digest_vote_batch(self, votes) -> np.ndarray:
+        """votes: list of (viewID, sequenceID, digest bytes, nodeID bytes, msgType)."""
+        n = len(votes)
+        v = np.array([x[0] for x in votes], np.int64)
+        q = np.array([x[1] for x in votes], np.int64)
+        mt = np.array([x[4] for x in votes], np.int64)
+        db, do, dl = self.pack([x[2] for x in votes])
+        nb, no, nl = self.pack([x[3] for x in votes])
+        out = np.zeros((max(n, 1), 32), np.uint8)
+        _check(self._L.pbftv_digest_vote_batch(self._h, n, v.ctypes.data, q.ctypes.data, db.ctypes.data,
+                                               do.ctypes.data, dl.ctypes.data, nb.ctypes.data, no.ctypes.data,
+                                               nl.ctypes.data, mt.ctypes.data, out.ctypes.data))
+        return out[:n]
+
+    def digest_reply_batch(self, replies) -> np.ndarray:
+        """replies: list of (viewID, timestamp, clientID bytes, nodeID bytes, result bytes)."""
+        n = len(replies)
+        v = np.array([x[0] for x in replies], np.int64)
+        t = np.array([x[1] for x in replies], np.int64)
+        cb, co, cl = self.pack([x[2] for x in replies])
+        nb, no, nl = self.pack([x[3] for x in replies])
+        rb, ro, rl = self.pack([x[4] for x in replies])
+        out = np.zeros((max(n, 1), 32), np.uint8)
+        _check(self._L.pbftv_digest_reply_batch(self._h, n, v.ctypes.data, t.ctypes.data, cb.ctypes.data,
+                                                co.ctypes.data, cl.ctypes.data, nb.ctypes.data, no.ctypes.data,
+                                                nl.ctypes.data, rb.ctypes.data, ro.ctypes.data, rl.ctypes.data,
+                                                out.ctypes.data))
         return out[:n]
 
     # ---- ecdsa

@@ -81,6 +81,17 @@ def test_hash_hex_and_request_digests(ver, digest_kats):
     assert [g.tobytes().hex() for g in got] == want
 
 
+def test_vote_and_reply_digests(ver, digest_kats):
+    votes = [(v["viewID"], v["sequenceID"], bytes.fromhex(v["digest"]), bytes.fromhex(v["nodeID"]), v["msgType"])
+             for v in digest_kats["votes"]]
+    got = ver.digest_vote_batch(votes)
+    assert [g.tobytes().hex() for g in got] == [v["digest_of_preimage"] for v in digest_kats["votes"]]
+    reps = [(r["viewID"], r["timestamp"], bytes.fromhex(r["clientID"]), bytes.fromhex(r["nodeID"]),
+             bytes.fromhex(r["result"])) for r in digest_kats["replies"]]
+    got = ver.digest_reply_batch(reps)
+    assert [g.tobytes().hex() for g in got] == [r["digest_of_preimage"] for r in digest_kats["replies"]]
+
+
 def test_sha256_dev_api(ver):
     rng = np.random.default_rng(11)
     msgs = [rng.bytes(int(l)) for l in rng.integers(256, 4097, 2048)]

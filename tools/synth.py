@@ -178,3 +178,73 @@ def sha_config5(n: int, lo: int = 256, hi: int = 4096, seed: int = 0x50424654):
     total = int(lengths.sum())
     data = rng.integers(0, 256, total + 64, dtype=np.uint8)
     return data, offsets, lengths
+
+
+NODES = [b"MainNode", b"ReplicaNode1", b"ReplicaNode2", b"ReplicaNode3"]  # pbft/network/node.go:60-65
+VIEW = 10000000000                                                         # node.go:55
+
+
+def config1_cluster(n_req: int = 1000, seed: int = 0x50424654):
+    """the reference's 4-node message pattern for n_req
+    requests.  Per request: 3 replica prepares each verified by 3 peers (9), 4
+    commits each verified by 3 peers (12), 4 replies verified by the primary (4)
+    = 25 signature checks over 11 distinct signed messages; every prepare/commit
+    also re-checks the request digest (reference: 20 digest recomputes)."""
+    sys_path_fix()
+    from simple_pbft_amd import pbftv as gojson  # host-only Go-JSON encoder of the product (no GPU)
+    gojson.request, gojson.vote, gojson.reply = gojson.gojson_request, gojson.gojson_vote, gojson.gojson_reply
+    s = Signer(4, seed)
+    reqs, votes, vote_sig, replies, reply_sig = [], [], [], [], []
+    checks = []  # (kind, index, receiver)
+    for i in range(n_req):
+        req = (1668519246 + i, b"client%d" % i, b"printf", 1668519247222762700 + 1000 * i)
+        reqs.append(req)
+        d = hashlib.sha256(gojson.request(*req)).hexdigest().encode()
+        for sender in (1, 2, 3):                       # prepares from the replicas
+            v = (VIEW, req[3], d, NODES[sender], 0)
+            votes.append(v)
+            vote_sig.append(s.sign(hashlib.sha256(gojson.vote(*v)).digest(), sender))
+            checks += [("vote", len(votes) - 1, r) for r in range(4) if r != sender]
+        for sender in range(4):                        # commits from every node
+            v = (VIEW, req[3], d, NODES[sender], 1)
+            votes.append(v)
+            vote_sig.append(s.sign(hashlib.sha256(gojson.vote(*v)).digest(), sender))
+            checks += [("vote", len(votes) - 1, r) for r in range(4) if r != sender]
+        for sender in range(4):                        # replies to the primary
+            rp = (VIEW, req[0], req[1], NODES[sender], b"Executed")
+            replies.append(rp)
+            reply_sig.append(s.sign(hashlib.sha256(gojson.reply(*rp)).digest(), sender))
+            checks.append(("reply", len(replies) - 1, 0))
+    pub = s.pub.copy()
+    s.close()
+    return pub, reqs, votes, np.frombuffer(b"".join(vote_sig), np.uint8).reshape(-1, 64), replies, \
+        np.frombuffer(b"".join(reply_sig), np.uint8).reshape(-1, 64), checks
+
+
+def certs(n_keys: int, per_cert: int, n_certs: int, seed: int):
+    """n_certs quorum certificates of per_cert votes over one digest each, from
+    distinct replicas of an n_keys committee (configs 2 and 3)."""
+    s = Signer(n_keys, seed)
+    rng = np.random.default_rng(seed)
+    H = np.zeros((n_certs * per_cert, 32), np.uint8)
+    S = np.zeros((n_certs * per_cert, 64), np.uint8)
+    K = np.zeros(n_certs * per_cert, np.uint32)
+    for c in range(n_certs):
+        h = rng.bytes(32)
+        signers = rng.choice(n_keys, per_cert, replace=False)
+        for j, k in enumerate(signers):
+            i = c * per_cert + j
+            H[i] = np.frombuffer(h, np.uint8)
+            S[i] = np.frombuffer(s.sign(h, int(k)), np.uint8)
+            K[i] = k
+    pub = s.pub.copy()
+    s.close()
+    return pub, H, S, K
+
+
+def sys_path_fix():
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
