@@ -395,8 +395,8 @@ def main():
                 out["cpu_openssl_standin"] = ost
             out["other_configs"] = {
                 "config1": run_config1(ver),
-                "config2": run_certs(ver, 4, 6, 10000, 2000,
-                                     "config2: n=4, 10k requests x (3 prepare + 3 commit) sigs = 60k in one launch"),
+                "config2": run_certs(ver, 4, 3, 20000, 4000,
+                                     "config2: n=4, 10k requests x (prepare QC + commit QC) x 3 sigs = 60k in one launch"),
                 "config3": run_certs(ver, 100, 67, 10000, 500,
                                      "config3: n=100 committee, 10k certificates x 67 sigs = 670k on one GPU"),
                 "config5": run_config5(ver),
