@@ -81,11 +81,12 @@ int pbftv_stream_sync(pbftv_ctx* ctx, int dev);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every
  * kernel launch while enabled.  kernel: 0 = ecdsa scalars, 1 = ecdsa comb,
- * 2 = sha256.  pbftv_kernel_time_ms synchronises the device's stream and
+ * 2 = sha256, 3 = ecdsa wave-per-signature (small batches).  pbftv_kernel_time_ms synchronises the device's stream and
  * returns the summed milliseconds and the launch count since the last reset. */
 #define PBFTV_K_ECDSA_SCALARS 0
 #define PBFTV_K_ECDSA_COMB 1
 #define PBFTV_K_SHA256 2
+#define PBFTV_K_ECDSA_WAVE 3
 int pbftv_set_kernel_timing(pbftv_ctx* ctx, int enable);
 int pbftv_kernel_time_ms(pbftv_ctx* ctx, int dev, int kernel, double* out_ms, uint64_t* out_launches);
 int pbftv_reset_kernel_times(pbftv_ctx* ctx);

@@ -40,6 +40,15 @@ hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, cons
 hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* flag, const uint8_t* sigs,
                              const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
                              uint8_t* bitmap, hipStream_t st);
+// latency path for small batches: one wave per signature (scalars, per-window
+// points, butterfly sum, check) in one launch.  Output: okbytes[i] (one byte per
+// signature) when okbytes != nullptr, else bit i of bitmap set/cleared by word
+// atomics (bitmap need not be zeroed; its word-aligned 4-byte span is touched).
+hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
+                             uint64_t n, const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
+                             const uint32_t* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st);
+// batches up to this size take the latency path (env PBFTV_WAVE_MAX overrides; 0 disables)
+uint64_t wave_path_max();
 
 // ---- SHA-256 (sha256_kernels.hip) ----
 // data must stay readable 4 bytes past every message end (device allocations are padded).

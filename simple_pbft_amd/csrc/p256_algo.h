@@ -20,6 +20,7 @@
 // (tests/cpp) only.
 #pragma once
 #include "fe29.h"
+#include "safegcd.h"
 
 namespace pbftv {
 
@@ -258,7 +259,7 @@ PBFTV_HD bool ecdsa_scalars(const uint32_t e_w[8], const uint32_t r_w[8], const 
   fe_from_words(s, s_w);
   fe_set(r2n, kR2N);
   fn_mul(sm, s, r2n);         // s * R
-  fn_inv_mont(w, sm);         // s^-1 * R
+  fn_inv_mont_gcd(w, sm);     // s^-1 * R
   fn_mul(t, e, w);            // e * s^-1   (e < 2^256 < 2n: Montgomery handles it)
   fn_canon(t, t);
   fe_to_words(u1_w, t);

@@ -1,14 +1,17 @@
 // p256_kernels.hip -- ECDSA-P256 batch verification kernels for gfx950.
 //
-// One signature per lane (64 per wave).  Three kernels:
-//   k_build_tables   key validation + fixed-base comb tables for G and every
-//                    registered key (one lane per (base, 8-bit window)).
-//   k_ecdsa_scalars  Go's range checks on (r, s), w = s^-1 mod n (Fermat),
-//                    u1 = e w, u2 = r w  -> 64 B of scalars per signature.
-//   k_ecdsa_comb     u1*G + u2*Q as two 33-step signed-digit combs (mixed
-//                    additions only), one complete addition, and the x-coordinate
-//                    check  X == r Z^2 (or (r+n) Z^2) -- no field inversion.
-//                    Writes the LSB-first accept bitmap via a wave ballot.
+// Throughput path: one signature per lane (64 per wave).
+//   k_tab_*          key validation + fixed-base comb tables for G and every
+//                    registered key (three-phase parallel build).
+//   k_ecdsa_scalars  Go's range checks on (r, s), w = s^-1 mod n (K signatures
+//                    per lane share one safegcd inversion), u1 = e w, u2 = r w
+//                    -> 64 B of scalars per signature.
+//   k_ecdsa_comb     u1*G + u2*Q as one joint signed-digit comb over the W-bit
+//                    tables (mixed additions only) and the x-coordinate check
+//                    X == r Z^2 (or (r+n) Z^2) -- no field inversion.  Writes
+//                    the LSB-first accept bitmap via a wave ballot.
+// Latency path (small batches, e.g. one quorum certificate): one WAVE per
+// signature, k_ecdsa_wave (see there).
 // Semantics: Go 1.19 crypto/ecdsa.Verify (see p256_algo.h); parity with the
 // oracle is tested in tests/test_gpu_parity.py.
 #include <hip/hip_runtime.h>
@@ -236,7 +239,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     okm |= (ok ? 1u : 0u) << j;
   }
   fe inv;
-  fn_inv_mont(inv, acc);
+  fn_inv_mont_gcd(inv, acc);
   for (int j = K - 1; j >= 0; --j) {
     const uint64_t i = lane + (uint64_t)j * L;
     const bool ok = (okm >> j) & 1u;
@@ -381,6 +384,150 @@ __global__ void __launch_bounds__(256, 2) k_ecdsa_comb(const uint4* __restrict__
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wave_base = i - lane;
   if (lane < 8 && wave_base + 8 * lane < n) bitmap[(wave_base >> 3) + lane] = (uint8_t)(m >> (8 * lane));
+}
+
+// ---------------------------------------------------------------------------
+// Latency path (small batches: a quorum certificate): ONE WAVE PER SIGNATURE.
+// The throughput kernels above run one signature per lane, so a lone
+// certificate is a single wave walking a 292-multiply inversion chain and 34
+// dependent mixed additions -- the whole latency is one wave's serial
+// instruction stream.  Here the wave splits that stream:
+//   * every lane computes the scalars redundantly (Go's range checks, then
+//     w = s^-1 by safegcd divsteps -- ~5x fewer dependent multiplies than
+//     Fermat -- u1 = e w, u2 = r w);
+//   * lane j takes window j: G entry of digit j of u1 plus Q entry of digit j
+//     of u2 (one mixed addition, complete);
+//   * the per-window points are summed by a butterfly over the lanes
+//     (ceil(log2(windows)) complete Jacobian additions, __shfl_xor);
+//   * lane 0 does the x-coordinate check.
+// One 64-thread block per signature, so the waves spread over every SIMD.
+__device__ __forceinline__ void shfl_xor_fe(fe& dst, const fe& src, int m) {
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) dst.v[l] = (uint32_t)__shfl_xor((int)src.v[l], m, 64);
+}
+
+// r = p + q, complete: infinity flags, doubling and cancellation handled.
+__device__ __forceinline__ void jac_add_complete(jac& r, bool& rinf, const jac& p, bool pinf, const jac& q,
+                                                 bool qinf) {
+  if (pinf || qinf) {
+    r = pinf ? q : p;
+    rinf = pinf && qinf;
+    return;
+  }
+  jac s;
+  const int st = jac_add(s, p, q);
+  if (st == 1) {
+    jac_double(r, p);
+    rinf = false;
+  } else {
+    r = s;
+    rinf = st == 2;
+  }
+}
+
+template <int WG, int WQ>
+__global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ hashes,
+                                                   const uint8_t* __restrict__ sigs,
+                                                   const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                   const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                                   const uint4* __restrict__ gtab, const uint4* __restrict__ qtabs,
+                                                   uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  constexpr int nW = nG > nQ ? nG : nQ;
+  static_assert(nW <= 64, "one lane per window");
+  const int j = threadIdx.x;
+  const uint64_t i = blockIdx.x;
+  bool ok = false;
+  uint32_t r[8], s[8];
+  if (sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s)) {  // wave-uniform branch
+    uint32_t e[8], u1[8], u2[8];
+    load_be256(hashes + 32 * i, e);
+    ecdsa_scalars(e, r, s, u1, u2);
+    // digit j of each scalar (the signed recoding carries across windows)
+    digit_stream<WG> s1;
+    digit_stream<WQ> s2;
+    PBFTV_UNROLL for (int k = 0; k < 8; ++k) { s1.w[k] = u1[k]; s2.w[k] = u2[k]; }
+    s1.carry = s2.carry = 0;
+    int d1 = 0, d2 = 0;
+    for (int k = 0; k < nW; ++k) {
+      const int a = k < nG ? s1.next() : 0, b = k < nQ ? s2.next() : 0;
+      if (k == j) { d1 = a; d2 = b; }
+    }
+    // this lane's point: G entry (+) Q entry
+    const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
+    jac P;
+    bool inf = true;
+    if (d1 != 0) {
+      uint4 eg[4];
+      uint32_t w16[16];
+      load_entry<WG>(gtab, j, d1, eg);
+      entry_words(eg, w16);
+      comb_add_entry<true>(P, inf, d1, w16);
+    }
+    if (d2 != 0) {
+      uint4 eq[4];
+      uint32_t w16[16];
+      load_entry<WQ>(qtab, j, d2, eq);
+      entry_words(eq, w16);
+      comb_add_entry<true>(P, inf, d2, w16);
+    }
+    // butterfly: after level m every lane holds the sum over its 2m-lane group
+#pragma unroll 1
+    for (int m = 1; m < nW; m <<= 1) {
+      jac Q;
+      shfl_xor_fe(Q.x, P.x, m);
+      shfl_xor_fe(Q.y, P.y, m);
+      shfl_xor_fe(Q.z, P.z, m);
+      const bool qinf = __shfl_xor((int)inf, m, 64) != 0;
+      jac S;
+      bool sinf;
+      jac_add_complete(S, sinf, P, inf, Q, qinf);
+      P = S;
+      inf = sinf;
+    }
+    ok = ecdsa_check(P, !inf, r);
+  }
+  if (j != 0) return;
+  if (okbytes) {
+    okbytes[i] = ok ? 1 : 0;
+    return;
+  }
+  // one bit of the LSB-first bitmap: set or clear it with a word atomic
+  // (other signatures' waves share the byte; no pre-zeroing needed)
+  uint8_t* byte = bitmap + (i >> 3);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(byte);
+  unsigned int* word = reinterpret_cast<unsigned int*>(a & ~(uintptr_t)3);
+  const unsigned int bit = 1u << (((unsigned)(a & 3) << 3) + (unsigned)(i & 7));
+  if (ok) atomicOr(word, bit);
+  else atomicAnd(word, ~bit);
+}
+
+template <int WG, int WQ>
+static void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
+                          const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab, const uint32_t* qtabs,
+                          uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
+  hipLaunchKernelGGL((k_ecdsa_wave<WG, WQ>), dim3((uint32_t)n), dim3(64), 0, st, hashes, sigs, key_idx, n, key_valid,
+                     nkeys, reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4*>(qtabs), bitmap,
+                     okbytes);
+}
+
+hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
+                             uint64_t n, const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
+                             const uint32_t* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+#define PBFTV_WAVE(G, Q) launch_wave_w<G, Q>(hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes, st)
+  if (wg == 16 && wq == 16) PBFTV_WAVE(16, 16);
+  else if (wg == 16 && wq == 12) PBFTV_WAVE(16, 12);
+  else if (wg == 16 && wq == 8) PBFTV_WAVE(16, 8);
+  else if (wg == 8 && wq == 8) PBFTV_WAVE(8, 8);
+  else return hipErrorInvalidValue;
+#undef PBFTV_WAVE
+  return hipGetLastError();
+}
+
+uint64_t wave_path_max() {
+  if (const char* e = getenv("PBFTV_WAVE_MAX")) return strtoull(e, nullptr, 10);
+  return 2048;
 }
 
 // signatures per lane in the scalar stage: enough lanes for ~2 waves per SIMD

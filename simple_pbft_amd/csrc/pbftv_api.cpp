@@ -66,6 +66,32 @@ struct DevBuf {
   }
 };
 
+// pinned, device-coherent host memory: kernels read inputs from and write
+// results to it directly (the small-batch latency path: no DMA copies)
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 1 << 16);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
@@ -77,13 +103,15 @@ struct Device {
   bool have_keys = false;
   // ecdsa scratch
   DevBuf hashes, sigs, key_idx, scal, flag, prefix, bitmap;
+  HostBuf stage;  // zero-copy inputs/outputs of the small-batch path
   // sha scratch
   DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
   // kernel timing (events recorded around launches while ctx timing is on)
   const bool* timing = nullptr;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[3];
-  double acc_ms[3] = {0, 0, 0};
-  uint64_t launches[3] = {0, 0, 0};
+  static constexpr int kKernels = 4;  // PBFTV_K_*
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[kKernels];
+  double acc_ms[kKernels] = {0, 0, 0, 0};
+  uint64_t launches[kKernels] = {0, 0, 0, 0};
 };
 
 // record start/stop events around one launch when timing is enabled
@@ -103,7 +131,7 @@ hipError_t timed(Device& d, int k, hipStream_t st, F launch) {
 }
 
 hipError_t collect_times(Device& d) {
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < Device::kKernels; ++k) {
     for (auto& pr : d.pending[k]) {
       hipError_t e = hipEventSynchronize(pr.second);
       if (e != hipSuccess) return e;
@@ -221,6 +249,7 @@ void pbftv_close(pbftv_ctx* ctx) {
                       &d->data, &d->offsets, &d->lengths, &d->order, &d->order_scratch, &d->digests, &d->expected,
                       &d->shabits})
       b->release();
+    d->stage.release();
     (void)hipStreamDestroy(d->stream);
   }
   delete ctx;
@@ -316,7 +345,7 @@ int pbftv_set_kernel_timing(pbftv_ctx* ctx, int enable) {
 
 int pbftv_kernel_time_ms(pbftv_ctx* ctx, int dev, int kernel, double* out_ms, uint64_t* out_launches) {
   Device* d = dev_of(ctx, dev);
-  if (!d || kernel < 0 || kernel > 2) return fail(PBFTV_EINVAL, "bad argument");
+  if (!d || kernel < 0 || kernel >= Device::kKernels) return fail(PBFTV_EINVAL, "bad argument");
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
   HIP_TRY(collect_times(*d));
@@ -331,7 +360,7 @@ int pbftv_reset_kernel_times(pbftv_ctx* ctx) {
     std::lock_guard<std::mutex> lk(dp->mu);
     HIP_TRY(hipSetDevice(dp->id));
     HIP_TRY(collect_times(*dp));
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < Device::kKernels; ++k) {
       dp->acc_ms[k] = 0;
       dp->launches[k] = 0;
     }
@@ -449,6 +478,13 @@ int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uin
 static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d_sigs, const uint32_t* d_key_idx,
                             uint64_t n, uint8_t* d_bitmap, hipStream_t st) {
   if (!d.have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  if (n <= pbftv::wave_path_max()) {
+    HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, st, [&] {
+      return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(),
+                                      d.nkeys, d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(), d_bitmap, nullptr, st);
+    }));
+    return PBFTV_OK;
+  }
   HIP_TRY(d.scal.ensure(n * 64));
   HIP_TRY(d.flag.ensure(n));
   HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
@@ -480,6 +516,29 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
   if (n && (!hashes || !sig_rs || !key_idx || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
   for (auto& dp : ctx->devs)
     if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  if (n && n <= pbftv::wave_path_max()) {
+    // latency path on the first device: inputs packed into pinned coherent
+    // host memory that the kernel reads directly, one byte per signature
+    // written back the same way -- one launch and one stream sync, no copies.
+    Device& d = *ctx->devs[0];
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    const size_t oh = 0, os = 32 * n, ok = 96 * n, oo = 100 * n;
+    HIP_TRY(d.stage.ensure(oo + n + 64));
+    uint8_t* st8 = d.stage.as<uint8_t>();
+    std::memcpy(st8 + oh, hashes, 32 * n);
+    std::memcpy(st8 + os, sig_rs, 64 * n);
+    std::memcpy(st8 + ok, key_idx, 4 * n);
+    HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
+      return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, st8 + oh, st8 + os, reinterpret_cast<uint32_t*>(st8 + ok), n,
+                                      d.key_valid.as<uint32_t>(), d.nkeys, d.gtab.as<uint32_t>(),
+                                      d.qtabs.as<uint32_t>(), nullptr, st8 + oo, d.stream);
+    }));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    std::memset(out_bitmap, 0, (n + 7) / 8);
+    for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((st8[oo + i] & 1u) << (i & 7));
+    return PBFTV_OK;
+  }
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
     const uint64_t m = s.hi - s.lo;
     std::lock_guard<std::mutex> lk(d.mu);

@@ -198,6 +198,7 @@ def verify_msg_batch(state_view: int, state_last_seq: int, req_digest: bytes, vi
 K_ECDSA_SCALARS = 0
 K_ECDSA_COMB = 1
 K_SHA256 = 2
+K_ECDSA_WAVE = 3
 
 
 class DeviceBuffer:

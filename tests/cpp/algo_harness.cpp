@@ -62,6 +62,16 @@ void h_fe_to_words(const uint32_t* a, uint32_t* w) {
   memcpy(x.v, a, 36);
   fe_to_words(w, x);
 }
+void h_inv_n_words(const uint32_t* x, uint32_t* out) { inv_mod_n_words(out, x); }
+
+void h_fn_inv_mont(const uint32_t* a, int use_gcd, uint32_t* r) {
+  fe x, y;
+  fe_set(x, a);
+  if (use_gcd) fn_inv_mont_gcd(y, x);
+  else fn_inv_mont(y, x);
+  std::memcpy(r, y.v, 36);
+}
+
 int h_scalars(const uint32_t* e, const uint32_t* r, const uint32_t* s, uint32_t* u1, uint32_t* u2) {
   return ecdsa_scalars(e, r, s, u1, u2) ? 1 : 0;
 }

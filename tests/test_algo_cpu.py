@@ -179,3 +179,36 @@ def test_comb_fast_and_checked_paths_agree(H):
             x = sum(int(v) << 32 * i for i, v in enumerate(out_a[:8]))
             y = sum(int(v) << 32 * i for i, v in enumerate(out_a[8:]))
             assert (x, y) == want
+
+
+# ---- safegcd inversion mod n (simple_pbft_amd/csrc/safegcd.h) ----------------
+def _w8(v):
+    return (ctypes.c_uint32 * 8)(*[(v >> 32 * i) & 0xFFFFFFFF for i in range(8)])
+
+
+def test_safegcd_inverse_mod_n(H):
+    rng = np.random.default_rng(0x5AFE)
+    xs = [1, 2, 3, N - 1, N - 2, (N - 1) // 2, 1 << 255, (1 << 256) % N, (1 << 128) - 1, 0xFFFFFFFF,
+          N >> 1, (N + 1) // 2, 3 ** 150 % N]
+    xs += [int.from_bytes(rng.bytes(32), "big") % N or 1 for _ in range(3000)]
+    xs += [1 << k for k in range(256)]
+    xs += [(1 << k) - 1 for k in range(1, 256)]
+    out = (ctypes.c_uint32 * 8)()
+    for x in xs:
+        H.h_inv_n_words(_w8(x), out)
+        got = sum(int(v) << 32 * i for i, v in enumerate(out))
+        assert got == pow(x, -1, N), hex(x)
+
+
+def test_safegcd_matches_fermat_montgomery(H):
+    rng = np.random.default_rng(7)
+    R = 1 << 261
+    H.h_fn_inv_mont.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    for _ in range(300):
+        x = int.from_bytes(rng.bytes(32), "big") % N or 5
+        xm = x * R % N
+        a, b = (ctypes.c_uint32 * 9)(), (ctypes.c_uint32 * 9)()
+        H.h_fn_inv_mont(limbs(xm), 1, a)
+        H.h_fn_inv_mont(limbs(xm), 0, b)
+        want = pow(x, -1, N) * R % N
+        assert val(a) % N == want and val(b) % N == want

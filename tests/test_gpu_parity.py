@@ -20,6 +20,15 @@ def ver():
     v.close()
 
 
+# Two ECDSA paths: "wave" (one wave per signature, batches <= PBFTV_WAVE_MAX)
+# and "lane" (one signature per lane: scalars + comb kernels).  Parity tests
+# run through both by moving the threshold.
+@pytest.fixture(params=["wave", "lane"])
+def path(request, monkeypatch):
+    monkeypatch.setenv("PBFTV_WAVE_MAX", "100000000" if request.param == "wave" else "0")
+    return request.param
+
+
 # ------------------------------------------------------------------ SHA-256
 def test_sha256_fixtures(ver, sha_fixtures):
     msgs, want = [], []
@@ -129,7 +138,7 @@ def test_register_keys_validity(ver, ecdsa_fixtures):
     assert valid.tolist() == [k["valid"] for k in ecdsa_fixtures["keys"]]
 
 
-def test_ecdsa_fixtures(ver, ecdsa_fixtures):
+def test_ecdsa_fixtures(ver, ecdsa_fixtures, path):
     keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
     ver.register_keys(keys)
     got = ver.verify_batch(hashes, sigs, kidx)
@@ -137,7 +146,7 @@ def test_ecdsa_fixtures(ver, ecdsa_fixtures):
     assert not bad, bad
 
 
-def test_ecdsa_fixtures_every_alignment(ver, ecdsa_fixtures):
+def test_ecdsa_fixtures_every_alignment(ver, ecdsa_fixtures, path):
     """Same vectors at every position of a wave / bitmap byte."""
     keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
     ver.register_keys(keys)
@@ -149,7 +158,7 @@ def test_ecdsa_fixtures_every_alignment(ver, ecdsa_fixtures):
         assert (ver.verify_batch(h, s, k) == e).all()
 
 
-def test_ecdsa_random_vs_oracle(ver, oracle_lib):
+def test_ecdsa_random_vs_oracle(ver, oracle_lib, path):
     keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=16, per_key=64, seed=99)
     rng = np.random.default_rng(5)
     n = len(kidx)
@@ -181,7 +190,7 @@ def test_ecdsa_random_vs_oracle(ver, oracle_lib):
 
 
 @pytest.mark.parametrize("gq", [(16, 16), (16, 12), (16, 8), (8, 8)])
-def test_ecdsa_every_table_width(oracle_lib, ecdsa_fixtures, gq, monkeypatch):
+def test_ecdsa_every_table_width(oracle_lib, ecdsa_fixtures, gq, path, monkeypatch):
     """Golden vectors + random corruptions vs the oracle for every comb geometry."""
     from simple_pbft_amd import Verifier
     monkeypatch.setenv("PBFTV_GBITS", str(gq[0]))
@@ -210,6 +219,7 @@ def test_ecdsa_scalar_batch_sizes(ver, oracle_lib, ecdsa_fixtures, k, monkeypatc
     reps = 9
     H, S, K, E = (np.tile(hashes, (reps, 1)), np.tile(sigs, (reps, 1)), np.tile(kidx, reps), np.tile(expect, reps))
     monkeypatch.setenv("PBFTV_SCALAR_BATCH", str(k))
+    monkeypatch.setenv("PBFTV_WAVE_MAX", "0")
     ver.register_keys(keys)
     got = ver.verify_batch(H, S, K)
     assert (got == E).all()
@@ -245,7 +255,7 @@ def test_ecdsa_no_keys_and_out_of_range(ecdsa_fixtures):
         assert not v.verify_batch(hashes, sigs, k).any()
 
 
-def test_qc_verify(ver, oracle_lib):
+def test_qc_verify(ver, oracle_lib, path):
     keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=4, per_key=3, seed=4)
     ver.register_keys(keys)
     bm, acc, ok = ver.qc_verify(hashes, sigs, kidx, quorum=3)
@@ -255,7 +265,8 @@ def test_qc_verify(ver, oracle_lib):
     assert acc == 2 and not ok and bm.tolist() == [False] * 10 + [True] * 2
 
 
-def test_ecdsa_dev_api(ver, ecdsa_fixtures):
+def test_ecdsa_dev_api(ver, ecdsa_fixtures, path):
+    from simple_pbft_amd.pbftv import K_ECDSA_COMB, K_ECDSA_WAVE
     keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
     ver.register_keys(keys)
     n = len(kidx)
@@ -267,10 +278,26 @@ def test_ecdsa_dev_api(ver, ecdsa_fixtures):
     ver.reset_kernel_times()
     ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
     ver.sync(0)
-    ms, cnt = ver.kernel_time_ms(0, 1)
+    ms, cnt = ver.kernel_time_ms(0, K_ECDSA_WAVE if path == "wave" else K_ECDSA_COMB)
     ver.set_kernel_timing(False)
     assert cnt == 1 and ms > 0
     got = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
     assert (got == expect).all()
     for b in (dh, ds, dk, db):
         b.free()
+
+
+def test_ecdsa_wave_path_edge_counts(ver, oracle_lib, monkeypatch):
+    """The wave path at batch sizes around its 8-signature blocks and at the
+    default threshold, against the oracle (1 in 5 corrupted)."""
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=6, per_key=400, seed=31)
+    sigs[::5, 33] ^= 0x40
+    ver.register_keys(keys)
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    for n in (1, 2, 7, 8, 9, 15, 16, 17, 67, 2047, 2048, 2049, 2400):
+        got = ver.verify_batch(hashes[:n], sigs[:n], kidx[:n])
+        assert (got == want[:n]).all(), n
