@@ -62,13 +62,17 @@ def macs_comb(gbits: int, qbits: int) -> float:
     return (nonzero(gbits) + nonzero(qbits) - 1) * MADD + CHECK
 
 
-INV_N = 292                                         # fn_inv_mont addition chain (p256_algo.h)
+# safegcd inversion (safegcd.h): at most 25 batches of 30 divsteps, each applying
+# its 2x2 matrix to (f, g) (36 signed 32x32 products) and (d, e) (54 incl. the
+# n multiples), plus one Montgomery product by R^3.  The divsteps themselves are
+# 32-bit shift/compare work, not MACs.
+INV_N_MACS = 25 * (36 + 54) + 162
 
 
 def macs_scalars(k: int) -> float:
     """k signatures per lane share one inversion (Montgomery's trick, p256_kernels.hip)."""
     per_sig = 7 if k > 1 else 4
-    return (per_sig + INV_N / k) * FN_MUL
+    return per_sig * FN_MUL + INV_N_MACS / k
 # v_mad_u64_u32 issue peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz (4-cycle wave64 issue);
 # measured 30.9 T lane-ops/s in profiles/r01_valu_microbench.txt
 MAD_PEAK = 256 * 4 * 16 * 2.4e9

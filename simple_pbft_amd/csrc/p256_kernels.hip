@@ -40,9 +40,13 @@ __device__ __forceinline__ void load_be256(const uint8_t* __restrict__ p, uint32
 template <int W>
 struct TabGeom {
   using G = CombGeom<W>;
-  static constexpr int CL = G::kEnt < 256 ? G::kEnt : 256;  // L table: (lo+1) B_i, lo < CL
-  static constexpr int NH = G::kEnt / CL;                   // H table: hi (CL B_i), 1 <= hi < NH
+  // L table: (lo+1) B_i, lo < CL; H table: hi (CL B_i), 1 <= hi < NH.  Up to
+  // W = 16 CL = 256; wider windows split E = CL * NH near sqrt(E) so neither
+  // phase-2 walk gets long (W = 20: 1024 x 512, W = 24: 4096 x 2048).
+  static constexpr int CL = G::kEnt < 256 ? G::kEnt : (W <= 16 ? 256 : 1 << (W / 2));
+  static constexpr int NH = G::kEnt / CL;
   static constexpr int PC = CL < 64 ? CL : 64;              // entries per phase-3 lane
+  static constexpr int SS = 4 * (CL > NH - 1 ? CL : NH - 1);  // phase-2 scratch slots per lane
 };
 
 __device__ __forceinline__ bool load_base(const uint32_t* __restrict__ keys_le, uint32_t key0, uint32_t b, int with_g,
@@ -85,7 +89,7 @@ __global__ void __launch_bounds__(64) k_tab_small(const uint32_t* __restrict__ b
   constexpr int nwin = CombGeom<W>::kWin;
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= nb * nwin) return;
-  fe* sc = scratch + (uint64_t)lane * 4 * T::CL;
+  fe* sc = scratch + (uint64_t)lane * T::SS;
   auto st = [&](int slot, const fe& v) { sc[slot] = v; };
   auto ld = [&](int slot, fe& v) { v = sc[slot]; };
   uint32_t bw[16];
@@ -99,17 +103,20 @@ __global__ void __launch_bounds__(64) k_tab_small(const uint32_t* __restrict__ b
   }
 }
 
-// phase 3: lane (b, win, hi, part) -> PC entries idx = hi*CL + part*PC + j of base b's table
+// phase 3: lane (b, win, hi, part) -> PC entries idx = hi*CL + part*PC + j of base b's table.
+// A launch covers global lanes [lane0, lane1); scratch is indexed by lane - lane0.
 template <int W>
 __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__ lbuf,
-                                                    const uint32_t* __restrict__ hbuf, uint32_t nb,
-                                                    uint32_t* __restrict__ tables, fe* __restrict__ scratch) {
+                                                    const uint32_t* __restrict__ hbuf, uint64_t lane0,
+                                                    uint64_t lane1, uint32_t* __restrict__ tables,
+                                                    fe* __restrict__ scratch) {
   using T = TabGeom<W>;
   using G = CombGeom<W>;
   constexpr int parts = T::CL / T::PC;
-  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t local = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t lane = lane0 + local;
   const uint64_t per_base = (uint64_t)G::kWin * T::NH * parts;
-  if (lane >= nb * per_base) return;
+  if (lane >= lane1) return;
   const uint32_t b = (uint32_t)(lane / per_base);
   uint32_t rem = (uint32_t)(lane % per_base);
   const uint32_t win = rem / (T::NH * parts);
@@ -122,7 +129,7 @@ __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__
     for (int i = 0; i < 16; ++i) hw[i] = hbuf[(bw * (T::NH - 1) + hi - 1) * 16 + i];
   uint32_t* out = tables + (uint64_t)b * G::kWords + ((uint64_t)win * G::kEnt + (uint64_t)hi * T::CL +
                                                       (uint64_t)part * T::PC) * 16;
-  fe* sc = scratch + (uint64_t)lane * 4 * T::PC;
+  fe* sc = scratch + local * 4 * T::PC;
   sums_chunk(out, T::PC, hi > 0, hw, L, [&](int slot, const fe& v) { sc[slot] = v; },
              [&](int slot, fe& v) { v = sc[slot]; });
 }
@@ -139,16 +146,14 @@ hipError_t build_tables_w(const uint32_t* keys_le, uint32_t key0, uint32_t nb, i
   hipLaunchKernelGGL(k_tab_small<W>, dim3((lanes12 + 63) / 64), dim3(64), 0, st,
                      reinterpret_cast<const uint32_t*>(sc.bases), nb, reinterpret_cast<uint32_t*>(sc.lbuf),
                      reinterpret_cast<uint32_t*>(sc.hbuf), reinterpret_cast<fe*>(sc.small_scratch));
-  // phase 3 in groups of bases so its scratch stays within sc.entry_lanes lanes
+  // phase 3 in slices of sc.entry_lanes lanes (its scratch is per lane)
   constexpr uint64_t per_base = (uint64_t)G::kWin * T::NH * (T::CL / T::PC);
-  const uint32_t group = (uint32_t)(sc.entry_lanes / per_base > 0 ? sc.entry_lanes / per_base : 1);
-  for (uint32_t b0 = 0; b0 < nb; b0 += group) {
-    const uint32_t g = nb - b0 < group ? nb - b0 : group;
-    const uint64_t lanes3 = (uint64_t)g * per_base;
-    hipLaunchKernelGGL(k_tab_entries<W>, dim3((uint32_t)((lanes3 + 63) / 64)), dim3(64), 0, st,
-                       reinterpret_cast<const uint32_t*>(sc.lbuf) + (uint64_t)b0 * G::kWin * T::CL * 16,
-                       reinterpret_cast<const uint32_t*>(sc.hbuf) + (uint64_t)b0 * G::kWin * (T::NH > 1 ? T::NH - 1 : 0) * 16,
-                       g, tables + (uint64_t)b0 * G::kWords, reinterpret_cast<fe*>(sc.entry_scratch));
+  const uint64_t total = (uint64_t)nb * per_base;
+  for (uint64_t l0 = 0; l0 < total; l0 += sc.entry_lanes) {
+    const uint64_t l1 = total - l0 < sc.entry_lanes ? total : l0 + sc.entry_lanes;
+    hipLaunchKernelGGL(k_tab_entries<W>, dim3((uint32_t)((l1 - l0 + 63) / 64)), dim3(64), 0, st,
+                       reinterpret_cast<const uint32_t*>(sc.lbuf), reinterpret_cast<const uint32_t*>(sc.hbuf), l0, l1,
+                       tables, reinterpret_cast<fe*>(sc.entry_scratch));
   }
   return hipGetLastError();
 }
@@ -161,20 +166,31 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
     z.bases = (size_t)nb * G::kWin * 64;
     z.lbuf = (size_t)nb * G::kWin * T::CL * 64;
     z.hbuf = (size_t)nb * G::kWin * (T::NH > 1 ? T::NH - 1 : 1) * 64;
-    z.small_scratch = (size_t)nb * G::kWin * 4 * T::CL * sizeof(fe);
-    const uint64_t per_base = (uint64_t)G::kWin * T::NH * (T::CL / T::PC);
-    const uint64_t lanes = per_base * nb < (uint64_t)(1 << 16) ? per_base * nb : (per_base > (1 << 16) ? per_base : (1 << 16));
-    z.entry_lanes = lanes;
-    z.entry_scratch = (size_t)lanes * 4 * T::PC * sizeof(fe);
+    z.small_scratch = (size_t)nb * G::kWin * T::SS * sizeof(fe);
+    const uint64_t total = (uint64_t)G::kWin * T::NH * (T::CL / T::PC) * nb;
+    const uint64_t cap = 1ull << 17;  // 128 Ki lanes x 9 KiB of scratch
+    z.entry_lanes = total < cap ? total : cap;
+    z.entry_scratch = (size_t)z.entry_lanes * 4 * T::PC * sizeof(fe);
   };
-  if (w == 8) fill(CombGeom<8>());
-  else if (w == 12) fill(CombGeom<12>());
-  else fill(CombGeom<16>());
+  switch (w) {
+    case 8: fill(CombGeom<8>()); break;
+    case 12: fill(CombGeom<12>()); break;
+    case 16: fill(CombGeom<16>()); break;
+    case 20: fill(CombGeom<20>()); break;
+    default: fill(CombGeom<24>()); break;
+  }
   return z;
 }
 
 size_t table_bytes(int w) {
-  return w == 8 ? CombGeom<8>::kBytes : w == 12 ? CombGeom<12>::kBytes : CombGeom<16>::kBytes;
+  switch (w) {
+    case 8: return CombGeom<8>::kBytes;
+    case 12: return CombGeom<12>::kBytes;
+    case 16: return CombGeom<16>::kBytes;
+    case 20: return CombGeom<20>::kBytes;
+    case 24: return CombGeom<24>::kBytes;
+    default: return 0;
+  }
 }
 
 hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g,
@@ -183,6 +199,8 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
     case 8: return build_tables_w<8>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     case 12: return build_tables_w<12>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     case 16: return build_tables_w<16>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    case 20: return build_tables_w<20>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    case 24: return build_tables_w<24>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -516,7 +534,10 @@ hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_
   if (n == 0) return hipSuccess;
   if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
 #define PBFTV_WAVE(G, Q) launch_wave_w<G, Q>(hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes, st)
-  if (wg == 16 && wq == 16) PBFTV_WAVE(16, 16);
+  if (wg == 24 && wq == 20) PBFTV_WAVE(24, 20);
+  else if (wg == 20 && wq == 20) PBFTV_WAVE(20, 20);
+  else if (wg == 24 && wq == 16) PBFTV_WAVE(24, 16);
+  else if (wg == 16 && wq == 16) PBFTV_WAVE(16, 16);
   else if (wg == 16 && wq == 12) PBFTV_WAVE(16, 12);
   else if (wg == 16 && wq == 8) PBFTV_WAVE(16, 8);
   else if (wg == 8 && wq == 8) PBFTV_WAVE(8, 8);
@@ -587,7 +608,10 @@ hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* fl
                              const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
                              uint8_t* bitmap, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (wg == 16 && wq == 16) launch_comb_w<16, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  if (wg == 24 && wq == 20) launch_comb_w<24, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 20 && wq == 20) launch_comb_w<20, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 24 && wq == 16) launch_comb_w<24, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 16 && wq == 16) launch_comb_w<16, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 16 && wq == 12) launch_comb_w<16, 12>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 16 && wq == 8) launch_comb_w<16, 8>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 8 && wq == 8) launch_comb_w<8, 8>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);

@@ -376,22 +376,42 @@ static int env_bits(const char* name, int dflt) {
   const char* e = getenv(name);
   if (!e) return dflt;
   const int v = atoi(e);
-  return (v == 8 || v == 12 || v == 16) ? v : dflt;
+  return (v == 8 || v == 12 || v == 16 || v == 20 || v == 24) ? v : dflt;
 }
 
+// Comb widths (G, keys) with instantiated kernels; the widest that fit win
+// (fewer windows = fewer mixed additions per verify).
+static bool combo_ok(int wg, int wq) {
+  static const int kCombos[][2] = {{24, 20}, {20, 20}, {24, 16}, {16, 16}, {16, 12}, {16, 8}, {8, 8}};
+  for (auto& c : kCombos)
+    if (c[0] == wg && c[1] == wq) return true;
+  return false;
+}
+
+// Key tables take up to min(free / 2, 128 GiB) of HBM by default (an MI355X
+// has 288 GB; 100 keys at 20-bit windows = 44 GB); PBFTV_TABLE_BUDGET_MB,
+// PBFTV_GBITS and PBFTV_QBITS override.
 static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
-  *wg = env_bits("PBFTV_GBITS", 16);
-  size_t budget = std::min<size_t>(16ull << 30, free_bytes / 4);
+  size_t budget = std::min<size_t>(128ull << 30, free_bytes / 2);
   if (const char* e = getenv("PBFTV_TABLE_BUDGET_MB")) budget = (size_t)atoll(e) << 20;
+  const uint64_t kk = k ? k : 1;
   int q = 8;
-  for (int w : {16, 12}) {
-    if ((size_t)k * pbftv::table_bytes(w) <= budget) {
+  for (int w : {20, 16, 12}) {
+    if (kk * pbftv::table_bytes(w) <= budget) {
       q = w;
       break;
     }
   }
-  *wq = env_bits("PBFTV_QBITS", q);
-  if (*wg == 8) *wq = 8;  // instantiated combos: (16,16) (16,12) (16,8) (8,8)
+  q = env_bits("PBFTV_QBITS", q);
+  const bool big_g = pbftv::table_bytes(24) * 4 <= free_bytes;
+  int g = env_bits("PBFTV_GBITS", (q >= 16 && big_g) ? 24 : 16);
+  if (!combo_ok(g, q)) {
+    if (q == 20) g = big_g ? 24 : 20;
+    else if (q == 16) g = (g == 24 && big_g) ? 24 : 16;
+    else if (!(g == 8 && q == 8)) g = 16;
+  }
+  *wg = g;
+  *wq = q;
 }
 
 static int build_tables(Device& d, int w, const uint32_t* d_keys, uint32_t nb, int with_g, uint32_t* valid,
@@ -433,7 +453,7 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     int wg, wq;
-    choose_bits(k, free_b + d.qtabs.cap, &wg, &wq);
+    choose_bits(k, free_b + d.qtabs.cap + d.gtab.cap, &wg, &wq);
     if (d.gbits != wg) {  // G table: once per context (and width)
       HIP_TRY(d.gtab.ensure(pbftv::table_bytes(wg)));
       DevBuf dummy;

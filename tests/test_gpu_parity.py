@@ -189,7 +189,7 @@ def test_ecdsa_random_vs_oracle(ver, oracle_lib, path):
     assert want.sum() > n // 2
 
 
-@pytest.mark.parametrize("gq", [(16, 16), (16, 12), (16, 8), (8, 8)])
+@pytest.mark.parametrize("gq", [(24, 20), (20, 20), (24, 16), (16, 16), (16, 12), (16, 8), (8, 8)])
 def test_ecdsa_every_table_width(oracle_lib, ecdsa_fixtures, gq, path, monkeypatch):
     """Golden vectors + random corruptions vs the oracle for every comb geometry."""
     from simple_pbft_amd import Verifier
