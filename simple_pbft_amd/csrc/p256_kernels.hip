@@ -369,10 +369,21 @@ __device__ bool comb2_dev_pass(jac& acc, const uint32_t u1[8], const uint32_t u2
 
 // The complete-addition rerun is a real call so its registers do not
 // inflate the fast path's allocation (it runs only for exceptional lanes).
+// It re-reads its inputs from memory and returns only the accept bit: no
+// local object's address crosses the call, so the fast path's accumulator
+// stays in registers (a jac passed by reference would live in scratch and
+// cost a 108-byte store + load per addition).
 template <int WG, int WQ>
-__device__ __noinline__ bool comb2_checked(jac& acc, const uint32_t u1[8], const uint32_t u2[8],
-                                           const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
-  return comb2_dev_pass<true, WG, WQ>(acc, u1, u2, gtab, qtab);
+__device__ __noinline__ bool comb2_checked_verify(const uint4* __restrict__ sp, const uint8_t* __restrict__ sig,
+                                                  const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
+  const uint4 a = sp[0], b = sp[1], c = sp[2], dd = sp[3];
+  const uint32_t u1[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const uint32_t u2[8] = {c.x, c.y, c.z, c.w, dd.x, dd.y, dd.z, dd.w};
+  jac R;
+  const bool fin = comb2_dev_pass<true, WG, WQ>(R, u1, u2, gtab, qtab);
+  uint32_t r[8];
+  load_be256(sig, r);
+  return ecdsa_check(R, fin, r);
 }
 
 template <int WG, int WQ>
@@ -391,11 +402,14 @@ __global__ void __launch_bounds__(256, 2) k_ecdsa_comb(const uint4* __restrict__
     const uint32_t u2[8] = {c.x, c.y, c.z, c.w, dd.x, dd.y, dd.z, dd.w};
     const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
     jac R;
-    bool fin = comb2_dev_pass<false, WG, WQ>(R, u1, u2, gtab, qtab);
-    if (fin && fe_is_zero(R.z)) fin = comb2_checked<WG, WQ>(R, u1, u2, gtab, qtab);  // exceptional step: redo
-    uint32_t r[8];
-    load_be256(sigs + 64 * i, r);
-    ok = ecdsa_check(R, fin, r);
+    const bool fin = comb2_dev_pass<false, WG, WQ>(R, u1, u2, gtab, qtab);
+    if (fin && fe_is_zero(R.z)) {
+      ok = comb2_checked_verify<WG, WQ>(sp, sigs + 64 * i, gtab, qtab);  // exceptional step: redo
+    } else {
+      uint32_t r[8];
+      load_be256(sigs + 64 * i, r);
+      ok = ecdsa_check(R, fin, r);
+    }
   }
   // LSB-first bitmap: wave ballot, lanes 0..7 store one byte each
   const unsigned long long m = __ballot(ok);
