@@ -427,11 +427,11 @@ __global__ void __launch_bounds__(256, 2) k_ecdsa_comb(const uint4* __restrict__
 //   * every lane computes the scalars redundantly (Go's range checks, then
 //     w = s^-1 by safegcd divsteps -- ~5x fewer dependent multiplies than
 //     Fermat -- u1 = e w, u2 = r w);
-//   * lane j takes window j: G entry of digit j of u1 plus Q entry of digit j
-//     of u2 (one mixed addition, complete);
-//   * the per-window points are summed by a butterfly over the lanes
-//     (ceil(log2(windows)) complete Jacobian additions, __shfl_xor);
-//   * lane 0 does the x-coordinate check.
+//   * quad q (lanes 4q..4q+3) takes window q: the G entry of digit q of u1
+//     plus the Q entry of digit q of u2, then a butterfly over the quads
+//     sums the windows (ceil(log2(windows)) Jacobian additions); the four
+//     lanes of a quad split each addition's multiplications (wave_sum_quads);
+//   * every lane does the x-coordinate check; lane 0 reports it.
 // One 64-thread block per signature, so the waves spread over every SIMD.
 __device__ __forceinline__ void shfl_xor_fe(fe& dst, const fe& src, int m) {
   PBFTV_UNROLL for (int l = 0; l < 9; ++l) dst.v[l] = (uint32_t)__shfl_xor((int)src.v[l], m, 64);
@@ -456,6 +456,222 @@ __device__ __forceinline__ void jac_add_complete(jac& r, bool& rinf, const jac& 
   }
 }
 
+// lane-per-window schedule (any window count): lane j adds its two entries
+// with complete formulas, then a butterfly of complete additions.  Used when
+// the windows outnumber the quads, and as the exact fallback of the quad
+// schedule below.
+template <int WG, int WQ>
+__device__ __forceinline__ void wave_sum_lanes(jac& P, bool& inf, const uint32_t u1[8], const uint32_t u2[8],
+                                               const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
+  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  constexpr int nW = nG > nQ ? nG : nQ;
+  const int j = threadIdx.x;
+  digit_stream<WG> s1;
+  digit_stream<WQ> s2;
+  PBFTV_UNROLL for (int k = 0; k < 8; ++k) { s1.w[k] = u1[k]; s2.w[k] = u2[k]; }
+  s1.carry = s2.carry = 0;
+  int d1 = 0, d2 = 0;
+  for (int k = 0; k < nW; ++k) {
+    const int a = k < nG ? s1.next() : 0, b = k < nQ ? s2.next() : 0;
+    if (k == j) { d1 = a; d2 = b; }
+  }
+  inf = true;
+  if (d1 != 0) {
+    uint4 eg[4];
+    uint32_t w16[16];
+    load_entry<WG>(gtab, j, d1, eg);
+    entry_words(eg, w16);
+    comb_add_entry<true>(P, inf, d1, w16);
+  }
+  if (d2 != 0) {
+    uint4 eq[4];
+    uint32_t w16[16];
+    load_entry<WQ>(qtab, j, d2, eq);
+    entry_words(eq, w16);
+    comb_add_entry<true>(P, inf, d2, w16);
+  }
+#pragma unroll 1
+  for (int m = 1; m < nW; m <<= 1) {
+    jac Q;
+    shfl_xor_fe(Q.x, P.x, m);
+    shfl_xor_fe(Q.y, P.y, m);
+    shfl_xor_fe(Q.z, P.z, m);
+    const bool qinf = __shfl_xor((int)inf, m, 64) != 0;
+    jac S;
+    bool sinf;
+    jac_add_complete(S, sinf, P, inf, Q, qinf);
+    P = S;
+    inf = sinf;
+  }
+}
+
+// ---- quad schedule: the four lanes of a quad share one point addition ------
+// Each step every lane of the quad does ONE field multiplication on operands
+// picked by its role (lane & 3), and the products are broadcast inside the
+// quad with DPP quad_perm moves (plain VALU, no LDS).  A Jacobian addition
+// (12M + 4S serially) becomes 5 multiplication steps, the affine + affine
+// first level 3 steps.
+template <int K>
+__device__ __forceinline__ void quad_bcast(fe& d, const fe& s) {
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l)
+    d.v[l] = (uint32_t)__builtin_amdgcn_mov_dpp((int)s.v[l], K * 0x55, 0xF, 0xF, false);
+}
+
+// Value selects by masks: a ?: between loads of two objects is turned into a
+// load through a selected pointer, which forces the objects into scratch.
+__device__ __forceinline__ uint32_t mask_of(bool c) { return 0u - (uint32_t)c; }
+
+__device__ __forceinline__ void quad_sel(fe& d, int role, const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
+  const uint32_t m0 = mask_of(role == 0), m1 = mask_of(role == 1), m2 = mask_of(role == 2), m3 = mask_of(role == 3);
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l)
+    d.v[l] = (a0.v[l] & m0) | (a1.v[l] & m1) | (a2.v[l] & m2) | (a3.v[l] & m3);
+}
+
+// d = c0 ? a : c1 ? b : c   (masks, see above)
+__device__ __forceinline__ void fe_sel3(fe& d, bool c0, const fe& a, bool c1, const fe& b, const fe& c) {
+  const uint32_t ma = mask_of(c0), mb = mask_of(!c0 && c1), mc = mask_of(!c0 && !c1);
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) d.v[l] = (a.v[l] & ma) | (b.v[l] & mb) | (c.v[l] & mc);
+}
+
+// product of the role's operand pair
+__device__ __forceinline__ void quad_mul(fe& p, int role, const fe& a0, const fe& b0, const fe& a1, const fe& b1,
+                                         const fe& a2, const fe& b2, const fe& a3, const fe& b3) {
+  fe a, b;
+  quad_sel(a, role, a0, a1, a2, a3);
+  quad_sel(b, role, b0, b1, b2, b3);
+  fe_mul(p, a, b);
+}
+
+// (gx, gy) + (qx, qy), both affine (mmadd-2007-bl); exc if x-coordinates meet.
+__device__ __forceinline__ void quad_mmadd(jac& r, bool& exc, int role, const fe& gx, const fe& gy, const fe& qx,
+                                           const fe& qy) {
+  fe h, t, rr, p, hh, r2, i4, jj, v, x3, a, b;
+  fe_sub(h, qx, gx);
+  fe_sub(t, qy, gy);
+  fe_add(rr, t, t);                                   // r = 2 (Y2 - Y1), lazy
+  exc = fe_is_zero(h);
+  quad_mul(p, role, h, h, rr, rr, h, h, rr, rr);      // HH, r^2
+  quad_bcast<0>(hh, p);
+  quad_bcast<1>(r2, p);
+  fe_mul_small(t, hh, 2);
+  fe_add(i4, t, t);                                   // I = 4 HH (lazy)
+  quad_mul(p, role, h, i4, gx, i4, h, i4, gx, i4);    // J = H I, V = X1 I
+  quad_bcast<0>(jj, p);
+  quad_bcast<1>(v, p);
+  fe_sub(t, r2, jj);
+  fe_add(a, v, v);
+  fe_sub(x3, t, a);                                   // X3 = r^2 - J - 2V
+  fe_sub(t, v, x3);
+  quad_mul(p, role, rr, t, gy, jj, rr, t, gy, jj);    // r (V - X3), Y1 J
+  quad_bcast<0>(a, p);
+  quad_bcast<1>(b, p);
+  fe_add(t, b, b);
+  fe_sub(r.y, a, t);                                  // Y3 = r (V - X3) - 2 Y1 J
+  fe_mul_small(r.z, h, 2);                            // Z3 = 2 H
+  r.x = x3;
+}
+
+// r = p + q (both finite Jacobian), the jac_add formulas in 5 steps; exc if H == 0.
+__device__ __forceinline__ void quad_jadd(jac& r, bool& exc, int role, const jac& P, const jac& Q) {
+  fe p, z1z1, z2z2, z1z2, u1, u2, t1, t2, h, s1, s2, hh, z3, rr, hhh, v, r2, x3, t, a, b;
+  quad_mul(p, role, P.z, P.z, Q.z, Q.z, P.z, Q.z, P.z, Q.z);
+  quad_bcast<0>(z1z1, p);
+  quad_bcast<1>(z2z2, p);
+  quad_bcast<2>(z1z2, p);
+  quad_mul(p, role, P.x, z2z2, Q.x, z1z1, Q.z, z2z2, P.z, z1z1);
+  quad_bcast<0>(u1, p);
+  quad_bcast<1>(u2, p);
+  quad_bcast<2>(t1, p);
+  quad_bcast<3>(t2, p);
+  fe_sub(h, u2, u1);
+  exc = fe_is_zero(h);
+  quad_mul(p, role, P.y, t1, Q.y, t2, h, h, z1z2, h);
+  quad_bcast<0>(s1, p);
+  quad_bcast<1>(s2, p);
+  quad_bcast<2>(hh, p);
+  quad_bcast<3>(z3, p);
+  fe_sub(rr, s2, s1);
+  quad_mul(p, role, hh, h, u1, hh, rr, rr, hh, h);
+  quad_bcast<0>(hhh, p);
+  quad_bcast<1>(v, p);
+  quad_bcast<2>(r2, p);
+  fe_sub(t, r2, hhh);
+  fe_add(a, v, v);
+  fe_sub(x3, t, a);                                   // X3 = r^2 - H^3 - 2 U1 H^2
+  fe_sub(t, v, x3);
+  quad_mul(p, role, rr, t, s1, hhh, rr, t, s1, hhh);
+  quad_bcast<0>(a, p);
+  quad_bcast<1>(b, p);
+  fe_sub(r.y, a, b);                                  // Y3 = r (V - X3) - S1 H^3
+  r.x = x3;
+  r.z = z3;                                           // Z3 = Z1 Z2 H
+}
+
+// quad q = window q: G entry + Q entry, then a butterfly over the quads.
+// exc reports a doubling / cancellation anywhere (the caller reruns the
+// signature with wave_sum_lanes).
+template <int WG, int WQ>
+__device__ __forceinline__ void wave_sum_quads(jac& P, bool& inf, bool& exc, const uint32_t u1[8],
+                                               const uint32_t u2[8], const uint4* __restrict__ gtab,
+                                               const uint4* __restrict__ qtab) {
+  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  constexpr int nW = nG > nQ ? nG : nQ;
+  static_assert(nW <= 16, "one quad per window");
+  const int role = threadIdx.x & 3, q = threadIdx.x >> 2;
+  digit_stream<WG> s1;
+  digit_stream<WQ> s2;
+  PBFTV_UNROLL for (int k = 0; k < 8; ++k) { s1.w[k] = u1[k]; s2.w[k] = u2[k]; }
+  s1.carry = s2.carry = 0;
+  int d1 = 0, d2 = 0;
+  for (int k = 0; k < nW; ++k) {
+    const int a = k < nG ? s1.next() : 0, b = k < nQ ? s2.next() : 0;
+    if (k == q) { d1 = a; d2 = b; }
+  }
+  uint4 eg[4], eq[4];
+  uint32_t w16[16];
+  load_entry<WG>(gtab, q < nG ? q : 0, d1, eg);
+  load_entry<WQ>(qtab, q < nQ ? q : 0, d2, eq);
+  fe gx, gy, qx, qy, ny;
+  entry_words(eg, w16);
+  entry_to_fe(gx, gy, w16);
+  if (d1 < 0) {
+    fe_neg_lazy(ny, gy);
+    fe_norm(gy, ny);
+  }
+  entry_words(eq, w16);
+  entry_to_fe(qx, qy, w16);
+  if (d2 < 0) {
+    fe_neg_lazy(ny, qy);
+    fe_norm(qy, ny);
+  }
+  jac S;
+  bool e0;
+  quad_mmadd(S, e0, role, gx, gy, qx, qy);            // every quad runs it; selected below
+  exc = d1 != 0 && d2 != 0 && e0;
+  inf = d1 == 0 && d2 == 0;
+  const bool both = d1 != 0 && d2 != 0, g_only = d1 != 0;
+  fe one;
+  fe_set(one, kOneP);
+  fe_sel3(P.x, both, S.x, g_only, gx, qx);
+  fe_sel3(P.y, both, S.y, g_only, gy, qy);
+  fe_sel3(P.z, both, S.z, true, one, one);
+#pragma unroll 1
+  for (int m = 1; m < nW; m <<= 1) {
+    jac Q;
+    shfl_xor_fe(Q.x, P.x, 4 * m);
+    shfl_xor_fe(Q.y, P.y, 4 * m);
+    shfl_xor_fe(Q.z, P.z, 4 * m);
+    const bool qinf = __shfl_xor((int)inf, 4 * m, 64) != 0;
+    bool e;
+    quad_jadd(S, e, role, P, Q);
+    exc = exc || (e && !inf && !qinf);
+    fe_sel3(P.x, inf, Q.x, qinf, P.x, S.x);
+    fe_sel3(P.y, inf, Q.y, qinf, P.y, S.y);
+    fe_sel3(P.z, inf, Q.z, qinf, P.z, S.z);
+    inf = inf && qinf;
+  }
+}
+
 template <int WG, int WQ>
 __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ hashes,
                                                    const uint8_t* __restrict__ sigs,
@@ -474,47 +690,15 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
     uint32_t e[8], u1[8], u2[8];
     load_be256(hashes + 32 * i, e);
     ecdsa_scalars(e, r, s, u1, u2);
-    // digit j of each scalar (the signed recoding carries across windows)
-    digit_stream<WG> s1;
-    digit_stream<WQ> s2;
-    PBFTV_UNROLL for (int k = 0; k < 8; ++k) { s1.w[k] = u1[k]; s2.w[k] = u2[k]; }
-    s1.carry = s2.carry = 0;
-    int d1 = 0, d2 = 0;
-    for (int k = 0; k < nW; ++k) {
-      const int a = k < nG ? s1.next() : 0, b = k < nQ ? s2.next() : 0;
-      if (k == j) { d1 = a; d2 = b; }
-    }
-    // this lane's point: G entry (+) Q entry
     const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
     jac P;
-    bool inf = true;
-    if (d1 != 0) {
-      uint4 eg[4];
-      uint32_t w16[16];
-      load_entry<WG>(gtab, j, d1, eg);
-      entry_words(eg, w16);
-      comb_add_entry<true>(P, inf, d1, w16);
-    }
-    if (d2 != 0) {
-      uint4 eq[4];
-      uint32_t w16[16];
-      load_entry<WQ>(qtab, j, d2, eq);
-      entry_words(eq, w16);
-      comb_add_entry<true>(P, inf, d2, w16);
-    }
-    // butterfly: after level m every lane holds the sum over its 2m-lane group
-#pragma unroll 1
-    for (int m = 1; m < nW; m <<= 1) {
-      jac Q;
-      shfl_xor_fe(Q.x, P.x, m);
-      shfl_xor_fe(Q.y, P.y, m);
-      shfl_xor_fe(Q.z, P.z, m);
-      const bool qinf = __shfl_xor((int)inf, m, 64) != 0;
-      jac S;
-      bool sinf;
-      jac_add_complete(S, sinf, P, inf, Q, qinf);
-      P = S;
-      inf = sinf;
+    bool inf;
+    if constexpr (nW <= 16) {
+      bool exc;
+      wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
+      if (__any(exc)) wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qtab);  // doubling somewhere: exact rerun
+    } else {
+      wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qtab);
     }
     ok = ecdsa_check(P, !inf, r);
   }

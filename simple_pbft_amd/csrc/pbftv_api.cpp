@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -539,7 +540,8 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
   if (n && n <= pbftv::wave_path_max()) {
     // latency path on the first device: inputs packed into pinned coherent
     // host memory that the kernel reads directly, one byte per signature
-    // written back the same way -- one launch and one stream sync, no copies.
+    // written back the same way and polled for (sentinel 0xFF) -- one launch,
+    // no copies, no stream synchronisation on the fast path.
     Device& d = *ctx->devs[0];
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
@@ -549,14 +551,30 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     std::memcpy(st8 + oh, hashes, 32 * n);
     std::memcpy(st8 + os, sig_rs, 64 * n);
     std::memcpy(st8 + ok, key_idx, 4 * n);
+    std::memset(st8 + oo, 0xFF, n);
     HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
       return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, st8 + oh, st8 + os, reinterpret_cast<uint32_t*>(st8 + ok), n,
                                       d.key_valid.as<uint32_t>(), d.nkeys, d.gtab.as<uint32_t>(),
                                       d.qtabs.as<uint32_t>(), nullptr, st8 + oo, d.stream);
     }));
-    HIP_TRY(hipStreamSynchronize(d.stream));
+    // every wave writes its byte after its last read of the inputs, so once
+    // all n bytes are in, the staging area is free for the next call
+    const volatile uint8_t* res = st8 + oo;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t next = 0; next < n;) {
+      if (res[next] != 0xFF) {
+        ++next;
+        continue;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        HIP_TRY(hipStreamSynchronize(d.stream));  // surfaces a kernel fault
+        for (uint64_t i = next; i < n; ++i)
+          if (res[i] == 0xFF) return fail(PBFTV_EDEVICE, "wave verify kernel did not report every signature");
+        break;
+      }
+    }
     std::memset(out_bitmap, 0, (n + 7) / 8);
-    for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((st8[oo + i] & 1u) << (i & 7));
+    for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((res[i] & 1u) << (i & 7));
     return PBFTV_OK;
   }
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {

@@ -112,3 +112,37 @@ def oracle_sign_pool(oracle_lib, n_keys: int, per_key: int, seed: int):
             if oracle_lib.oracle_ecdsa_p256_sign(hashes[i].ctypes.data, privs[kidx[i]], kb, sigs[i].ctypes.data):
                 break
     return keys, hashes, sigs, kidx
+
+
+def crafted_exceptional():
+    """Valid signatures with chosen (u1, u2) under the key Q = G: pick u1, u2,
+    R = (u1 + u2) G, r = x(R) mod n, s = r / u2, e = u1 s (the verifier then
+    recomputes exactly u1, u2).  The (u1, u2) pairs make table points meet
+    inside the sum -- at the first (G entry + Q entry) level and at the
+    butterfly / comb levels -- for every window geometry, so every doubling
+    and cancellation path (and the exact reruns behind them) is exercised.
+    Expected bits come from the oracle restatement (parity pinned by the
+    golden fixtures)."""
+    from oracle import p256
+    N = p256.N
+    pairs = [(5, 5), (77 << 24, 77 << 24), (3 << 20, 3 << 20), (1 << 16, 1 << 16), (9 << 8, 9 << 8),
+             ((1 << 23) + 1, (1 << 23) + 1), (12345, 2 * 12345), (1 << 20, (1 << 24) - (1 << 20)),
+             ((5 << 40) + 7, (5 << 40) + 7), ((3 << 20) + (1 << 24), 3 << 20), (2, N - 2),
+             (0xABCDEF << 48, 0xABCDEF << 48), (N - 1, N - 1), (N - 5, 5 + (1 << 30))]
+    H, S, K, E = [], [], [], []
+    for u1, u2 in pairs:
+        R = p256.scalar_mult((u1 + u2) % N, p256.G)
+        if R is None:  # u1 + u2 == 0: any well-formed signature with these scalars is rejected
+            r = 1
+        else:
+            r = R[0] % N
+        s = r * pow(u2, -1, N) % N
+        e = u1 * s % N
+        h = e.to_bytes(32, "big")
+        for rr, ss, hh in ((r, s, h), (r ^ 2, s, h)):
+            H.append(np.frombuffer(hh, np.uint8))
+            S.append(np.frombuffer(rr.to_bytes(32, "big") + ss.to_bytes(32, "big"), np.uint8))
+            K.append(0)
+            E.append(p256.verify(hh, rr, ss, p256.GX, p256.GY))
+    key = np.frombuffer(p256.GX.to_bytes(32, "big") + p256.GY.to_bytes(32, "big"), np.uint8)[None, :]
+    return key, np.stack(H), np.stack(S), np.array(K, np.uint32), np.array(E, bool)

@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT, fixture_arrays, oracle_sign_pool
+from conftest import crafted_exceptional, ROOT, fixture_arrays, oracle_sign_pool
 
 P = 0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF
 N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
@@ -179,6 +179,17 @@ def test_comb_fast_and_checked_paths_agree(H):
             x = sum(int(v) << 32 * i for i, v in enumerate(out_a[:8]))
             y = sum(int(v) << 32 * i for i, v in enumerate(out_a[8:]))
             assert (x, y) == want
+
+
+def test_pipeline_crafted_exceptional_sums(H):
+    """Chosen-(u1, u2) signatures under Q = G whose comb sums hit doublings and
+    cancellations (tests/conftest.py crafted_exceptional) on the 8-bit tables."""
+    key, hashes, sigs, kidx, expect = crafted_exceptional()
+    g, tabs, valid = _tables(H, key)
+    assert valid == [1]
+    for i in range(len(kidx)):
+        got = H.h_verify(hashes[i].tobytes(), sigs[i].tobytes(), g, tabs[0], 1)
+        assert bool(got) == expect[i], i
 
 
 # ---- safegcd inversion mod n (simple_pbft_amd/csrc/safegcd.h) ----------------

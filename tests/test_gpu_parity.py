@@ -7,7 +7,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import fixture_arrays, oracle_sign_pool
+from conftest import crafted_exceptional, fixture_arrays, oracle_sign_pool
 
 pytestmark = pytest.mark.gpu
 
@@ -301,3 +301,16 @@ def test_ecdsa_wave_path_edge_counts(ver, oracle_lib, monkeypatch):
     for n in (1, 2, 7, 8, 9, 15, 16, 17, 67, 2047, 2048, 2049, 2400):
         got = ver.verify_batch(hashes[:n], sigs[:n], kidx[:n])
         assert (got == want[:n]).all(), n
+
+
+@pytest.mark.parametrize("gq", [(24, 20), (20, 20), (24, 16), (16, 16), (16, 8), (8, 8)])
+def test_ecdsa_crafted_exceptional_sums(gq, path, monkeypatch):
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_GBITS", str(gq[0]))
+    monkeypatch.setenv("PBFTV_QBITS", str(gq[1]))
+    key, H, S, K, E = crafted_exceptional()
+    assert E.sum() >= 10  # the crafted ones verify, the r-flipped ones do not
+    with Verifier() as v:
+        v.register_keys(key)
+        assert v.table_config()[:2] == gq
+        assert (v.verify_batch(H, S, K) == E).all()
