@@ -179,8 +179,84 @@ PBFTV_HD void fe_mont_reduce_p(fe& r, uint64_t t[18]) {
   r.v[8] = (uint32_t)(t[16] >> 29);
 }
 
-// r = a * b * 2^-261 mod p (M-type)
+// One Montgomery digit step at column i (the body of fe_mont_reduce_p's loop).
+PBFTV_HD void fe_mont_digit_p(uint64_t t[18], int i, uint32_t c9, uint32_t c18, uint32_t c21, uint32_t c24) {
+  const uint32_t m = (uint32_t)t[i] & kMask29;
+  t[i + 1] += t[i] >> 29;
+  t[i + 3] += (uint64_t)m * c9;
+  t[i + 6] += (uint64_t)m * c18;
+  t[i + 7] += (uint64_t)(m ^ kMask29) * c21;
+  t[i + 8] += (uint64_t)m * c24;
+}
+
+PBFTV_HD void fe_mont_out_p(fe& r, uint64_t t[18]) {
+  PBFTV_UNROLL for (int j = 9; j < 16; ++j) {
+    r.v[j - 9] = (uint32_t)t[j] & kMask29;
+    t[j + 1] += t[j] >> 29;
+  }
+  r.v[7] = (uint32_t)t[16] & kMask29;
+  r.v[8] = (uint32_t)(t[16] >> 29);
+}
+
+// r = a * b * 2^-261 mod p (M-type).  The reduction is interleaved with the
+// products: column i is final once product row i is in, so digit step i is
+// issued right after that row and its serial carry overlaps the next row's
+// independent multiply-adds (tools/fmul_bench.hip: 772 vs 856 SIMD-cycles per
+// wave at 2 waves/SIMD).  Same sums in the same columns as
+// fe_mul_rows_then_reduce -- identical results.
 PBFTV_HD void fe_mul(fe& r, const fe& a, const fe& b) {
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
+                 c24 = opaque_u32(1u << 24);
+  uint64_t t[18];
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * b.v[j];
+    fe_mont_digit_p(t, i, c9, c18, c21, c24);
+  }
+  fe_mont_out_p(r, t);
+}
+
+// r = (a b + c d) * 2^-261 mod p (M-type): two products summed in the columns,
+// ONE Montgomery reduction.  Column bound: a, b limbs < 2^29 and c < 2^30,
+// d < 2^29 give < 9 (2^58 + 2^59) < 2^62.8 before the reduction's additions.
+PBFTV_HD void fe_mul2_add(fe& r, const fe& a, const fe& b, const fe& c, const fe& d) {
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
+                 c24 = opaque_u32(1u << 24);
+  uint64_t t[18];
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * b.v[j];
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)c.v[i] * d.v[j];
+    fe_mont_digit_p(t, i, c9, c18, c21, c24);
+  }
+  fe_mont_out_p(r, t);
+}
+
+// fe_sqr with the reduction interleaved (after square row i columns <= 2i+1
+// are final); measured no faster than fe_sqr, kept for tools/fmul_bench.hip.
+PBFTV_HD void fe_sqr_il(fe& r, const fe& a) {
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
+                 c24 = opaque_u32(1u << 24);
+  uint64_t t[18];
+  uint32_t a2[9];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) a2[i] = a.v[i] << 1;
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    t[2 * i] += (uint64_t)a.v[i] * a.v[i];
+    PBFTV_UNROLL for (int j = i + 1; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * a2[j];
+    if (2 * i < 9) fe_mont_digit_p(t, 2 * i, c9, c18, c21, c24);
+    if (2 * i + 1 < 9) fe_mont_digit_p(t, 2 * i + 1, c9, c18, c21, c24);
+  }
+  fe_mont_out_p(r, t);
+}
+
+// r = a * b * 2^-261 mod p (M-type), all products first, then the reduction
+// (kept as the reference schedule for tools/fmul_bench.hip; fe_mul below
+// interleaves the two and is ~10 % faster on gfx950)
+PBFTV_HD void fe_mul_rows_then_reduce(fe& r, const fe& a, const fe& b) {
   uint64_t t[18];
   PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
   PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
@@ -234,13 +310,13 @@ PBFTV_HD bool fe_equal(const fe& a, const fe& b) {
 // ---------------------------------------------------------------------------
 // scalar field mod n: Montgomery (R = 2^261), generic quotient digit.
 // Values kept < 2^257 (limbs < 2^29 after each multiply); inputs limbs < 2^30.
+// Digit step i is interleaved right after product row i (column i is final
+// then), as in fe_mul.
 PBFTV_HD void fn_mul(fe& r, const fe& a, const fe& b) {
   uint64_t t[18];
   PBFTV_UNROLL for (int k = 0; k < 18; ++k) t[k] = 0;
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * b.v[j];
-  }
-  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     const uint32_t m = ((uint32_t)t[i] * kNPrime) & kMask29;
     PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)m * kN[j];
     t[i + 1] += t[i] >> 29;

@@ -7,8 +7,8 @@
 //                    per lane share one safegcd inversion), u1 = e w, u2 = r w
 //                    -> 64 B of scalars per signature.
 //   k_ecdsa_comb     u1*G + u2*Q as one joint signed-digit comb over the W-bit
-//                    tables (mixed additions only) and the x-coordinate check
-//                    X == r Z^2 (or (r+n) Z^2) -- no field inversion.  Writes
+//                    tables (XYZZ mixed additions only) and the x-coordinate check
+//                    X == r ZZ (or (r+n) ZZ) -- no field inversion.  Writes
 //                    the LSB-first accept bitmap via a wave ballot.
 // Latency path (small batches, e.g. one quorum certificate): one WAVE per
 // signature, k_ecdsa_wave (see there).
@@ -17,11 +17,16 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.h"
 #include "p256_algo.h"
 
 namespace pbftv {
+
+#ifndef PBFTV_COMB_WAVES
+#define PBFTV_COMB_WAVES 2  // min waves per SIMD for k_ecdsa_comb (register budget 512 / this)
+#endif
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -324,7 +329,11 @@ struct digit_stream {
 template <int W>
 __device__ __forceinline__ void load_entry(const uint4* __restrict__ tab, int win, int d, uint4 e[4]) {
   const int idx = (d < 0 ? -d : d) - 1;
+#ifdef PBFTV_EXP_L2TAB  // timing experiment only: lookups confined to 4 MiB per window (results wrong)
+  const uint4* p = tab + ((uint64_t)win * CombGeom<W>::kEnt + (idx < 0 ? 0 : idx & 0xFFFF)) * 4;
+#else
   const uint4* p = tab + ((uint64_t)win * CombGeom<W>::kEnt + (idx < 0 ? 0 : idx)) * 4;
+#endif
   e[0] = p[0]; e[1] = p[1]; e[2] = p[2]; e[3] = p[3];
 }
 
@@ -334,8 +343,16 @@ __device__ __forceinline__ void entry_words(const uint4 e[4], uint32_t ew[16]) {
   }
 }
 
-template <bool kCheck, int WG, int WQ>
-__device__ bool comb2_dev_pass(jac& acc, const uint32_t u1[8], const uint32_t u2[8],
+// Acc = xyzz: the unchecked fast pass (comb_add_entry_xyzz); Acc = jac with
+// kCheck: the complete-addition rerun (comb_add_entry<true>).
+template <bool kCheck, class Acc>
+__device__ __forceinline__ void comb_dev_add(Acc& acc, bool& inf, int d, const uint32_t ew[16]) {
+  if constexpr (kCheck) comb_add_entry<true>(acc, inf, d, ew);
+  else comb_add_entry_xyzz(acc, inf, d, ew);
+}
+
+template <bool kCheck, int WG, int WQ, class Acc>
+__device__ bool comb2_dev_pass(Acc& acc, const uint32_t u1[8], const uint32_t u2[8],
                                const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
   constexpr int nW = nG > nQ ? nG : nQ;
@@ -361,8 +378,8 @@ __device__ bool comb2_dev_pass(jac& acc, const uint32_t u1[8], const uint32_t u2
       d2 = s2.next();
       load_entry<WQ>(qtab, i + 1, d2, eq);
     }
-    if (c1 != 0) comb_add_entry<kCheck>(acc, inf, c1, wg);
-    if (c2 != 0) comb_add_entry<kCheck>(acc, inf, c2, wq);
+    if (c1 != 0) comb_dev_add<kCheck>(acc, inf, c1, wg);
+    if (c2 != 0) comb_dev_add<kCheck>(acc, inf, c2, wq);
   }
   return !inf;
 }
@@ -386,34 +403,137 @@ __device__ __noinline__ bool comb2_checked_verify(const uint4* __restrict__ sp, 
   return ecdsa_check(R, fin, r);
 }
 
+// Joint comb schedule: step j of the nG + nQ additions takes the G entry of
+// window j/2 (j even) and the Q entry (j odd) while both tables have windows
+// left, then the longer table's remaining windows.
 template <int WG, int WQ>
-__global__ void __launch_bounds__(256, 2) k_ecdsa_comb(const uint4* __restrict__ scal, const uint8_t* __restrict__ flag,
+struct CombSteps {
+  static constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  static constexpr int nMin = nG < nQ ? nG : nQ;
+  static constexpr int nD = nG + nQ;
+  // LDS digit storage: d - 1 fits int16 for W <= 16 (d in [-(2^15 - 1), 2^15])
+  using Digit = std::conditional_t<(WG > 16 || WQ > 16), int, short>;
+  __host__ __device__ static constexpr bool is_q(int j) { return j < 2 * nMin ? (j & 1) != 0 : nQ > nG; }
+  __host__ __device__ static constexpr int win(int j) { return j < 2 * nMin ? j >> 1 : j - nMin; }
+};
+
+// y = d < 0 ? 2p - y : y, lazily (limbs < 2^30: a valid fe_mul input) -- a
+// per-lane mask select, no carry chain and no divergence.
+__device__ __forceinline__ void fe_cneg_lazy(fe& y, bool neg) {
+  const uint32_t m = 0u - (uint32_t)neg;
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) y.v[l] = y.v[l] ^ ((y.v[l] ^ (kP2Borrow[l] - y.v[l])) & m);
+}
+
+template <int W>
+__device__ __forceinline__ const uint4* entry_ptr(const uint4* __restrict__ tab, int win, int d) {
+  const int idx = (d < 0 ? -d : d) - 1;
+#ifdef PBFTV_EXP_SMALLTAB  // timing experiment only: 256 KiB footprint per table (results wrong)
+  return tab + (uint64_t)(idx < 0 ? 0 : idx & 0xFFF) * 4;
+#else
+  return tab + ((uint64_t)win * CombGeom<W>::kEnt + (idx < 0 ? 0 : idx)) * 4;
+#endif
+}
+
+// Async copy of this lane's 64-B entry into sent[.][t]: four 16-B
+// global_load_lds, each writing the wave's 64 lanes contiguously at the
+// wave-uniform base &sent[k][t & ~63].
+__device__ __forceinline__ void issue_entry_lds(uint4 (*sent)[256], uint32_t t, const uint4* p) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this lane's reads of the slot are done
+  const uint32_t wb = t & ~63u;
+  __builtin_amdgcn_global_load_lds(p + 0, &sent[0][wb], 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(p + 1, &sent[1][wb], 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(p + 2, &sent[2][wb], 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(p + 3, &sent[3][wb], 16, 0, 0);
+}
+
+__device__ __forceinline__ void read_entry_lds(uint4 (*sent)[256], uint32_t t, uint32_t ew[16]) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies have landed
+  uint4 e[4];
+  PBFTV_UNROLL for (int k = 0; k < 4; ++k) e[k] = sent[k][t];
+  entry_words(e, ew);
+}
+
+template <int WG, int WQ>
+__global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint4* __restrict__ scal, const uint8_t* __restrict__ flag,
                                                        const uint8_t* __restrict__ sigs,
                                                        const uint32_t* __restrict__ key_idx, uint64_t n,
                                                        const uint4* __restrict__ gtab,
                                                        const uint4* __restrict__ qtabs,
                                                        uint8_t* __restrict__ bitmap) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  using S = CombSteps<WG, WQ>;
+  // signed digits of u1 / u2 in step order, one column per thread: recoded once
+  // in the prologue so the main loop holds no 256-bit digit shift registers
+  __shared__ typename S::Digit sdig[S::nD][256];
+  // the table entry of the next step, streamed global -> LDS (no VGPRs held
+  // while it is in flight): piece k of thread t at sent[k][t]
+  __shared__ uint4 sent[4][256];
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + t;
+  const bool active = i < n && flag[i];
   bool ok = false;
-  if (i < n && flag[i]) {
+  if (active) {
     const uint4* sp = scal + 4 * i;
-    const uint4 a = sp[0], b = sp[1], c = sp[2], dd = sp[3];
-    const uint32_t u1[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const uint32_t u2[8] = {c.x, c.y, c.z, c.w, dd.x, dd.y, dd.z, dd.w};
+    {
+      const uint4 a = sp[0], b = sp[1], c = sp[2], dd = sp[3];
+      digit_stream<WG> s1;
+      digit_stream<WQ> s2;
+      s1.w[0] = a.x; s1.w[1] = a.y; s1.w[2] = a.z; s1.w[3] = a.w;
+      s1.w[4] = b.x; s1.w[5] = b.y; s1.w[6] = b.z; s1.w[7] = b.w;
+      s2.w[0] = c.x; s2.w[1] = c.y; s2.w[2] = c.z; s2.w[3] = c.w;
+      s2.w[4] = dd.x; s2.w[5] = dd.y; s2.w[6] = dd.z; s2.w[7] = dd.w;
+      s1.carry = s2.carry = 0;
+      PBFTV_UNROLL for (int j = 0; j < S::nD; ++j)
+        sdig[j][t] = (typename S::Digit)((S::is_q(j) ? s2.next() : s1.next()) - 1);
+    }
+#ifdef PBFTV_EXP_SMALLTAB
+    const uint4* qtab = qtabs;
+#else
     const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
-    jac R;
-    const bool fin = comb2_dev_pass<false, WG, WQ>(R, u1, u2, gtab, qtab);
-    if (fin && fe_is_zero(R.z)) {
+#endif
+    xyzz R;
+    bool inf = true;
+    int d = (int)sdig[0][t] + 1;
+    issue_entry_lds(sent, t, entry_ptr<WG>(gtab, 0, d));
+#pragma unroll 1
+    for (int j = 0; j < S::nD; ++j) {
+      uint32_t w16[16];
+      read_entry_lds(sent, t, w16);
+      const int dc = d;
+      if (j + 1 < S::nD) {  // next step's entry streams into LDS during this addition
+        d = (int)sdig[j + 1][t] + 1;
+        issue_entry_lds(sent, t, S::is_q(j + 1) ? entry_ptr<WQ>(qtab, S::win(j + 1), d)
+                                                : entry_ptr<WG>(gtab, S::win(j + 1), d));
+      }
+      if (dc != 0) {
+        fe x, y;
+        entry_to_fe(x, y, w16);
+        fe_cneg_lazy(y, dc < 0);
+        if (inf) {
+          R.x = x;
+          fe_norm(R.y, y);
+          fe_set(R.zz, kOneP);
+          fe_set(R.zzz, kOneP);
+          inf = false;
+        } else {
+#ifdef PBFTV_EXP_NOMADD  // timing experiment only: memory path without the additions (results wrong)
+          PBFTV_UNROLL for (int l = 0; l < 9; ++l) { R.x.v[l] ^= x.v[l]; R.y.v[l] += y.v[l]; }
+#else
+          xyzz_madd(R, x, y);
+#endif
+        }
+      }
+    }
+    if (!inf && fe_is_zero(R.zz)) {
       ok = comb2_checked_verify<WG, WQ>(sp, sigs + 64 * i, gtab, qtab);  // exceptional step: redo
     } else {
       uint32_t r[8];
       load_be256(sigs + 64 * i, r);
-      ok = ecdsa_check(R, fin, r);
+      ok = ecdsa_check(R, !inf, r);
     }
   }
   // LSB-first bitmap: wave ballot, lanes 0..7 store one byte each
   const unsigned long long m = __ballot(ok);
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = t & 63u;
   const uint64_t wave_base = i - lane;
   if (lane < 8 && wave_base + 8 * lane < n) bitmap[(wave_base >> 3) + lane] = (uint8_t)(m >> (8 * lane));
 }

@@ -14,7 +14,7 @@ import re
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpbftv.so")
+LIB_PATH = os.environ.get("PBFTV_LIB") or os.path.join(HERE, "libpbftv.so")  # PBFTV_LIB: experiment builds only
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "pbftv.h")
 
 PBFTV_OK = 0

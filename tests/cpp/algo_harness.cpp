@@ -156,19 +156,28 @@ int h_verify_w(int w, const uint8_t* hash, const uint8_t* rs, const uint32_t* gt
   be32_to_le_words(rs, r);
   be32_to_le_words(rs + 32, s);
   if (!ecdsa_scalars(e, r, s, u1, u2)) return 0;
-  jac R;
-  bool fin = false;
+  bool ok = false;
   auto run = [&](auto geom) {
     constexpr int W = decltype(geom)::kW;
     auto lg = [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + ((uint64_t)win * CombGeom<W>::kEnt + idx) * 16, 64); };
     auto lq = [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + ((uint64_t)win * CombGeom<W>::kEnt + idx) * 16, 64); };
-    fin = comb2_mult<W, W>(R, u1, u2, lg, lq);
+    ok = comb2_verify<W, W>(u1, u2, r, lg, lq);
   };
   if (w == 8) run(CombGeom<8>());
   else if (w == 10) run(CombGeom<10>());
   else if (w == 12) run(CombGeom<12>());
   else return -1;
-  return ecdsa_check(R, fin, r) ? 1 : 0;
+  return ok ? 1 : 0;
+}
+
+// XYZZ mixed addition on raw limbs: acc = x||y||zz||zzz (36 words), pt = x||y (18 words).
+void h_xyzz_madd(uint32_t* acc, const uint32_t* pt) {
+  xyzz A;
+  fe x, y;
+  memcpy(A.x.v, acc, 36); memcpy(A.y.v, acc + 9, 36); memcpy(A.zz.v, acc + 18, 36); memcpy(A.zzz.v, acc + 27, 36);
+  memcpy(x.v, pt, 36); memcpy(y.v, pt + 9, 36);
+  xyzz_madd(A, x, y);
+  memcpy(acc, A.x.v, 36); memcpy(acc + 9, A.y.v, 36); memcpy(acc + 18, A.zz.v, 36); memcpy(acc + 27, A.zzz.v, 36);
 }
 
 // u * G via the joint comb (u2 = 0), unchecked (0) or complete-addition (1)
@@ -206,11 +215,12 @@ int h_verify(const uint8_t* hash, const uint8_t* rs, const uint32_t* gtab, const
   be32_to_le_words(rs, r);
   be32_to_le_words(rs + 32, s);
   if (!ecdsa_scalars(e, r, s, u1, u2)) return 0;
-  jac R;
-  const bool fin = comb2_mult(
-      R, u1, u2, [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64); },
-      [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64); });
-  return ecdsa_check(R, fin, r) ? 1 : 0;
+  return comb2_verify(
+             u1, u2, r,
+             [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64); },
+             [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + ((uint64_t)win * kEntries + idx) * kEntryWords, 64); })
+             ? 1
+             : 0;
 }
 
 }  // extern "C"

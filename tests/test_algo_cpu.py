@@ -223,3 +223,57 @@ def test_safegcd_matches_fermat_montgomery(H):
         H.h_fn_inv_mont(limbs(xm), 0, b)
         want = pow(x, -1, N) * R % N
         assert val(a) % N == want and val(b) % N == want
+
+
+# ---- XYZZ mixed addition (p256_algo.h xyzz_madd, the throughput comb's step) ---
+def test_xyzz_madd_chain_values_and_bounds(H):
+    """A chain of 60 madd-2008-s additions from a random XYZZ start: every
+    intermediate (X/ZZ, Y/ZZZ) equals the big-integer sum, limbs stay within
+    the fe29.h invariants (X, Y: N-type from fe_sub; ZZ, ZZZ: M-type), and
+    adding the accumulator's own point or its negative gives ZZ == ZZZ == 0."""
+    from oracle import p256
+    rng = np.random.default_rng(7)
+    A = ctypes.c_uint32 * 36
+    Pt = ctypes.c_uint32 * 18
+
+    def mont(v):
+        return v * R % P
+
+    def unmont(v):
+        return v * pow(R, -1, P) % P
+
+    def to_acc(pt, z):
+        x, y = pt
+        vals = [mont(x * z * z % P), mont(y * z * z * z % P), mont(z * z % P), mont(z * z * z % P)]
+        return A(*[w for v in vals for w in limbs(v)])
+
+    def from_acc(acc):
+        x, y, zz, zzz = (unmont(val(acc[9 * k:9 * k + 9]) % P) for k in range(4))
+        assert zz != 0 and zzz != 0
+        return x * pow(zz, -1, P) % P, y * pow(zzz, -1, P) % P
+
+    cur = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+    acc = to_acc(cur, int(rng.integers(2, 2 ** 62)))
+    # 2p in the borrow form of fe_neg_lazy (p256_consts.h kP2Borrow)
+    p2b = [0x3ffffffe, 0x3ffffffe, 0x3ffffffe, 0x200003fe, 0x1fffffff, 0x1fffffff, 0x2007ffff, 0x3fbfffff, 0x01fffffe]
+    assert val(p2b) == 2 * P
+    for step in range(60):
+        q = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+        if step % 2:  # a negative comb digit: y2 = 2p - y lazily, limbs < 2^30 (k_ecdsa_comb fe_cneg_lazy)
+            ly = [b - a for a, b in zip(limbs(mont(q[1])), p2b)]
+            H.h_xyzz_madd(acc, Pt(*limbs(mont(q[0])), *ly))
+            q = (q[0], (P - q[1]) % P)
+        else:
+            H.h_xyzz_madd(acc, Pt(*limbs(mont(q[0])), *limbs(mont(q[1]))))
+        cur = p256.point_add(cur, q)
+        assert from_acc(acc) == cur, step
+        for k in range(4):
+            l = acc[9 * k:9 * k + 9]
+            assert all(x < (1 << 29) for x in l), (step, k)
+            assert val(l) < (2 ** 256 + 2 ** 237 if k == 0 else M_BOUND), (step, k)
+    for neg in (False, True):
+        x, y = from_acc(acc)
+        y = (P - y) % P if neg else y
+        a2 = A(*acc)
+        H.h_xyzz_madd(a2, Pt(*limbs(mont(x)), *limbs(mont(y))))
+        assert val(a2[18:27]) % P == 0 and val(a2[27:36]) % P == 0

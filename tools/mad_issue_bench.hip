@@ -1,0 +1,106 @@
+// v_mad_u64_u32 issue-cost microbenchmark for gfx950: does the (unused) SGPR
+// carry-out of VOP3b v_mad_u64_u32 serialise back-to-back issue?  Blocks of
+// 16 independent multiply-adds with one shared carry-out pair vs 8 rotated
+// pairs, plus a dependent chain and plain 32-bit adds, at 1..8 waves/SIMD
+// (occupancy limited by dynamic LDS).  Measurement tool for DESIGN.md §3.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mad_issue_bench.hip -o tools/mad_issue_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+#define M1(i, S) "v_mad_u64_u32 %[x" #i "], " S ", %[a], %[b], %[x" #i "]\n\t"
+#define SAME "s[40:41]"
+#define BODY_SAME M1(0, SAME) M1(1, SAME) M1(2, SAME) M1(3, SAME) M1(4, SAME) M1(5, SAME) M1(6, SAME) M1(7, SAME) \
+                  M1(8, SAME) M1(9, SAME) M1(10, SAME) M1(11, SAME) M1(12, SAME) M1(13, SAME) M1(14, SAME) M1(15, SAME)
+#define BODY_ROT M1(0, "s[40:41]") M1(1, "s[42:43]") M1(2, "s[44:45]") M1(3, "s[46:47]") M1(4, "s[48:49]") \
+                 M1(5, "s[50:51]") M1(6, "s[52:53]") M1(7, "s[54:55]") M1(8, "s[40:41]") M1(9, "s[42:43]") \
+                 M1(10, "s[44:45]") M1(11, "s[46:47]") M1(12, "s[48:49]") M1(13, "s[50:51]") M1(14, "s[52:53]") \
+                 M1(15, "s[54:55]")
+#define C1 "v_mad_u64_u32 %[x0], s[40:41], %[a], %[b], %[x0]\n\t"
+#define BODY_CHAIN C1 C1 C1 C1 C1 C1 C1 C1 C1 C1 C1 C1 C1 C1 C1 C1
+#define L1(i) "v_lshl_add_u64 %[x" #i "], %[x" #i "], 0, %[x15]\n\t"
+#define BODY_LSHL L1(0) L1(1) L1(2) L1(3) L1(4) L1(5) L1(6) L1(7) L1(8) L1(9) L1(10) L1(11) L1(12) L1(13) L1(14) L1(0)
+#define A1(i) "v_add_u32 %[y" #i "], %[y" #i "], %[a]\n\t"
+#define BODY_ADD A1(0) A1(1) A1(2) A1(3) A1(4) A1(5) A1(6) A1(7) A1(0) A1(1) A1(2) A1(3) A1(4) A1(5) A1(6) A1(7)
+#define P1(i) "v_add_co_u32 %[y" #i "], vcc, %[y" #i "], %[a]\n\tv_addc_co_u32 %[z" #i "], vcc, %[z" #i "], 0, vcc\n\t"
+#define BODY_ADDC P1(0) P1(1) P1(2) P1(3) P1(4) P1(5) P1(6) P1(7)
+#define X1(i) "v_mad_u64_u32 %[x" #i "], s[40:41], %[a], %[b], %[x" #i "]\n\tv_add_u32 %[y" #i "], %[y" #i "], %[a]\n\t"
+#define BODY_MIX X1(0) X1(1) X1(2) X1(3) X1(4) X1(5) X1(6) X1(7)
+
+#define OPS_X [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [x4] "+v"(x[4]), [x5] "+v"(x[5]), \
+  [x6] "+v"(x[6]), [x7] "+v"(x[7]), [x8] "+v"(x[8]), [x9] "+v"(x[9]), [x10] "+v"(x[10]), [x11] "+v"(x[11]), \
+  [x12] "+v"(x[12]), [x13] "+v"(x[13]), [x14] "+v"(x[14]), [x15] "+v"(x[15])
+#define OPS_Y [y0] "+v"(y[0]), [y1] "+v"(y[1]), [y2] "+v"(y[2]), [y3] "+v"(y[3]), [y4] "+v"(y[4]), [y5] "+v"(y[5]), \
+  [y6] "+v"(y[6]), [y7] "+v"(y[7]), [z0] "+v"(z[0]), [z1] "+v"(z[1]), [z2] "+v"(z[2]), [z3] "+v"(z[3]), \
+  [z4] "+v"(z[4]), [z5] "+v"(z[5]), [z6] "+v"(z[6]), [z7] "+v"(z[7])
+#define CLOB "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "vcc"
+
+enum { SAMEC, ROTC, CHAIN, LSHL, ADD, ADDC, MIX, NV };
+static const char* kName[NV] = {"mad_u64 16 indep, one sdst", "mad_u64 16 indep, 8 sdst rot", "mad_u64 dep chain",
+                                "lshl_add_u64 indep", "add_u32 indep", "add_co+addc pairs", "mad_u64 + add_u32 alt"};
+
+template <int V>
+__global__ void __launch_bounds__(256) kb(uint32_t* out, int iters, uint32_t seed) {
+  extern __shared__ uint32_t pad[];
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x + seed;
+  uint64_t x[16];
+  uint32_t y[8], z[8];
+  for (int j = 0; j < 16; ++j) x[j] = (uint64_t)t * (j + 3);
+  for (int j = 0; j < 8; ++j) { y[j] = t * (j + 5); z[j] = t ^ j; }
+  const uint32_t a = t ^ 0x9e3779b9u, b = t * 7u;
+  for (int i = 0; i < iters; ++i) {
+    if constexpr (V == SAMEC) asm volatile(BODY_SAME : OPS_X : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == ROTC) asm volatile(BODY_ROT : OPS_X : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == CHAIN) asm volatile(BODY_CHAIN : OPS_X : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == LSHL) asm volatile(BODY_LSHL : OPS_X : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == ADD) asm volatile(BODY_ADD : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == ADDC) asm volatile(BODY_ADDC : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == MIX) asm volatile(BODY_MIX : OPS_X, OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+  }
+  uint32_t r = 0;
+  for (int j = 0; j < 16; ++j) r ^= (uint32_t)x[j] ^ (uint32_t)(x[j] >> 32);
+  for (int j = 0; j < 8; ++j) r ^= y[j] ^ z[j];
+  if (threadIdx.x == 0) pad[0] = r;
+  __syncthreads();
+  out[blockIdx.x * 256 + threadIdx.x] = r ^ pad[0];
+}
+
+template <int V>
+static void run(uint32_t* out, int wps) {
+  const int blocks = 256 * 8 * 2, iters = 2048;
+  const size_t lds = 160 * 1024 / wps - 512;
+  CHECK(hipFuncSetAttribute((const void*)kb<V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(kb<V>, dim3(blocks), dim3(256), lds, 0, out, 8, 1u);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(kb<V>, dim3(blocks), dim3(256), lds, 0, out, iters, 2u);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double waves = blocks * 4.0, instr = waves * iters * 16.0;
+  printf("%-30s waves/SIMD=%d  %6.2f SIMD-cycles per wave-instruction\n", kName[V], wps,
+         ms * 1e-3 * 2.4e9 * 1024.0 / instr);
+}
+
+int main() {
+  uint32_t* out;
+  CHECK(hipMalloc(&out, 256 * 8 * 2 * 256 * 4));
+  for (int w : {1, 2, 4, 8}) {
+    run<SAMEC>(out, w);
+    run<ROTC>(out, w);
+    run<CHAIN>(out, w);
+    run<LSHL>(out, w);
+    run<ADD>(out, w);
+    run<ADDC>(out, w);
+    run<MIX>(out, w);
+  }
+  return 0;
+}
