@@ -45,9 +45,9 @@ METRIC = "sig verifies/sec at 1/2/4/8 MI355X; p50 quorum-cert verify latency"
 # (one v_mad_u64_u32).  fe_mul 81, fe_sqr 45, fn_mul 81 + 81 (n-reduction).
 N_ORDER = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
 FE_MUL, FE_SQR, FN_MUL = 81, 45, 162
-MADD = 7 * FE_MUL + 4 * FE_SQR                     # madd-2007-bl
+MADD = 8 * FE_MUL + 2 * FE_SQR                     # XYZZ madd-2008-s (p256_algo.h xyzz_madd)
 JADD = 12 * FE_MUL + 4 * FE_SQR                    # add-2007-bl (final complete add)
-CHECK = FE_SQR + 2 * FE_MUL                         # X == r Z^2 test (+ rare r + n retry)
+CHECK = 2 * FE_MUL                                  # X == r ZZ test: r to Montgomery form, r ZZ
 
 
 def macs_comb(gbits: int, qbits: int) -> float:

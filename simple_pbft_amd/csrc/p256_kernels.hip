@@ -182,6 +182,7 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
     case 12: fill(CombGeom<12>()); break;
     case 16: fill(CombGeom<16>()); break;
     case 20: fill(CombGeom<20>()); break;
+    case 22: fill(CombGeom<22>()); break;
     default: fill(CombGeom<24>()); break;
   }
   return z;
@@ -193,6 +194,7 @@ size_t table_bytes(int w) {
     case 12: return CombGeom<12>::kBytes;
     case 16: return CombGeom<16>::kBytes;
     case 20: return CombGeom<20>::kBytes;
+    case 22: return CombGeom<22>::kBytes;
     case 24: return CombGeom<24>::kBytes;
     default: return 0;
   }
@@ -205,6 +207,7 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
     case 12: return build_tables_w<12>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     case 16: return build_tables_w<16>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     case 20: return build_tables_w<20>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    case 22: return build_tables_w<22>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     case 24: return build_tables_w<24>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     default: return hipErrorInvalidValue;
   }
@@ -852,7 +855,9 @@ hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_
   if (n == 0) return hipSuccess;
   if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
 #define PBFTV_WAVE(G, Q) launch_wave_w<G, Q>(hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes, st)
-  if (wg == 24 && wq == 20) PBFTV_WAVE(24, 20);
+  if (wg == 24 && wq == 22) PBFTV_WAVE(24, 22);
+  else if (wg == 24 && wq == 24) PBFTV_WAVE(24, 24);
+  else if (wg == 24 && wq == 20) PBFTV_WAVE(24, 20);
   else if (wg == 20 && wq == 20) PBFTV_WAVE(20, 20);
   else if (wg == 24 && wq == 16) PBFTV_WAVE(24, 16);
   else if (wg == 16 && wq == 16) PBFTV_WAVE(16, 16);
@@ -926,7 +931,9 @@ hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* fl
                              const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
                              uint8_t* bitmap, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (wg == 24 && wq == 20) launch_comb_w<24, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  if (wg == 24 && wq == 22) launch_comb_w<24, 22>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 24 && wq == 24) launch_comb_w<24, 24>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 24 && wq == 20) launch_comb_w<24, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 20 && wq == 20) launch_comb_w<20, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 24 && wq == 16) launch_comb_w<24, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 16 && wq == 16) launch_comb_w<16, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);

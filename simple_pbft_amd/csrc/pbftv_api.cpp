@@ -377,27 +377,34 @@ static int env_bits(const char* name, int dflt) {
   const char* e = getenv(name);
   if (!e) return dflt;
   const int v = atoi(e);
-  return (v == 8 || v == 12 || v == 16 || v == 20 || v == 24) ? v : dflt;
+  return (v == 8 || v == 12 || v == 16 || v == 20 || v == 22 || v == 24) ? v : dflt;
 }
 
 // Comb widths (G, keys) with instantiated kernels; the widest that fit win
 // (fewer windows = fewer mixed additions per verify).
 static bool combo_ok(int wg, int wq) {
-  static const int kCombos[][2] = {{24, 20}, {20, 20}, {24, 16}, {16, 16}, {16, 12}, {16, 8}, {8, 8}};
+  static const int kCombos[][2] = {{24, 24}, {24, 22}, {24, 20}, {20, 20}, {24, 16},
+                                   {16, 16}, {16, 12}, {16, 8},  {8, 8}};
   for (auto& c : kCombos)
     if (c[0] == wg && c[1] == wq) return true;
   return false;
 }
 
-// Key tables take up to min(free / 2, 128 GiB) of HBM by default (an MI355X
-// has 288 GB; 100 keys at 20-bit windows = 44 GB); PBFTV_TABLE_BUDGET_MB,
-// PBFTV_GBITS and PBFTV_QBITS override.
+// HBM kept free for batch buffers and other users of the device.
+constexpr size_t kTableReserve = 64ull << 30;
+
+// Key tables may take all of the device's free HBM but kTableReserve and the
+// 24-bit G table (an MI355X has 288 GB: 4 keys at 24-bit windows = 23.6 GB,
+// 100 keys at 22-bit = 161 GB, 1000 keys at 16-bit = 35 GB);
+// PBFTV_TABLE_BUDGET_MB, PBFTV_GBITS and PBFTV_QBITS override.
 static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
-  size_t budget = std::min<size_t>(128ull << 30, free_bytes / 2);
+  const size_t g24 = pbftv::table_bytes(24);
+  size_t budget = free_bytes > kTableReserve + g24 ? free_bytes - kTableReserve - g24 : 0;
+  budget = std::max(budget, free_bytes / 8);
   if (const char* e = getenv("PBFTV_TABLE_BUDGET_MB")) budget = (size_t)atoll(e) << 20;
   const uint64_t kk = k ? k : 1;
   int q = 8;
-  for (int w : {20, 16, 12}) {
+  for (int w : {24, 22, 20, 16, 12}) {
     if (kk * pbftv::table_bytes(w) <= budget) {
       q = w;
       break;
@@ -407,7 +414,9 @@ static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
   const bool big_g = pbftv::table_bytes(24) * 4 <= free_bytes;
   int g = env_bits("PBFTV_GBITS", (q >= 16 && big_g) ? 24 : 16);
   if (!combo_ok(g, q)) {
-    if (q == 20) g = big_g ? 24 : 20;
+    if (q >= 22 && !big_g) q = 20;  // (20|24, 22|24) need the 24-bit G table
+    if (q >= 22) g = 24;
+    else if (q == 20) g = big_g ? 24 : 20;
     else if (q == 16) g = (g == 24 && big_g) ? 24 : 16;
     else if (!(g == 8 && q == 8)) g = 16;
   }

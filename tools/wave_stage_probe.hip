@@ -10,9 +10,9 @@
 
 using namespace pbftv;
 
-constexpr int kStages = 7;
+constexpr int kStages = 9;
 
-__global__ void probe(const uint32_t* in, uint64_t* ticks, uint32_t* sink, int reps) {
+__global__ void probe(const uint32_t* in, uint64_t* ticks, uint32_t* sink, int reps, uint32_t lane_mask) {
   uint32_t e[8], r[8], s[8];
   for (int i = 0; i < 8; ++i) {
     e[i] = in[i];
@@ -64,6 +64,22 @@ __global__ void probe(const uint32_t* in, uint64_t* ticks, uint32_t* sink, int r
     P = R;
   }
   t[7] = wall_clock64();
+  for (int k = 0; k < reps; ++k) {  // 7: safegcd on per-lane (VALU) operands
+    uint32_t w[8], sv[8];
+    for (int q = 0; q < 8; ++q) sv[q] = s[q] ^ (threadIdx.x & lane_mask);
+    sv[1] ^= k;
+    inv_mod_n_words(w, sv);
+    acc += w[2];
+  }
+  t[8] = wall_clock64();
+  for (int k = 0; k < reps; ++k) {  // 8: safegcd on readfirstlane'd (SALU) operands
+    uint32_t w[8], sv[8];
+    for (int q = 0; q < 8; ++q) sv[q] = __builtin_amdgcn_readfirstlane(s[q] ^ (threadIdx.x & lane_mask));
+    sv[1] ^= k;
+    inv_mod_n_words(w, sv);
+    acc += w[2];
+  }
+  t[9] = wall_clock64();
   if (threadIdx.x == 0) {
     for (int i = 0; i < kStages; ++i) ticks[i] = t[i + 1] - t[i];
   }
@@ -86,13 +102,15 @@ int main() {
   hipMalloc(&d_sink, 4 * 64);
   hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice);
   const int reps = 20;
-  hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, d_in, d_t, d_sink, 2);  // warm
-  hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, d_in, d_t, d_sink, reps);
+  hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, d_in, d_t, d_sink, 2, 0u);  // warm
+  hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, d_in, d_t, d_sink, reps, 0u);
   uint64_t t[kStages];
   hipMemcpy(t, d_t, sizeof(t), hipMemcpyDeviceToHost);
   const char* names[kStages] = {"ecdsa_scalars (safegcd)", "inv_mod_n safegcd", "fn_inv_mont Fermat",
-                                "fe_mul", "jac_add", "jac_madd<true>", "jac_double"};
-  const double per[kStages] = {1.0 * reps, 1.0 * reps, 1.0 * reps, 100.0 * reps, 1.0 * reps, 1.0 * reps, 1.0 * reps};
+                                "fe_mul", "jac_add", "jac_madd<true>", "jac_double", "inv_mod_n VALU operands",
+                                "inv_mod_n SALU operands"};
+  const double per[kStages] = {1.0 * reps, 1.0 * reps, 1.0 * reps, 100.0 * reps, 1.0 * reps, 1.0 * reps, 1.0 * reps,
+                                1.0 * reps, 1.0 * reps};
   printf("{\"wall_clock_khz\": %d", rate_khz);
   for (int i = 0; i < kStages; ++i) printf(", \"%s_us\": %.3f", names[i], t[i] / per[i] * 1e3 / rate_khz);
   printf("}\n");
