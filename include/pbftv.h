@@ -167,14 +167,15 @@ int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const 
 /* Register the replica public keys (k * 64 B, X||Y big-endian); replaces any
  * previous table.  out_valid[j] = 1 if key j is a valid P-256 point (0 <= X,Y
  * < p and on the curve); signatures naming an invalid key always fail.  Builds
- * the per-key fixed-base comb tables on every device (34 MiB per key at the
- * default 16-bit windows; see pbftv_table_config). */
+ * the per-key fixed-base comb tables on every device (W-bit windows: 1.61 GB
+ * per key at W = 22, 436 MB at 20, 34 MiB at 16; see pbftv_table_config). */
 int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid);
 
-/* Comb-table geometry chosen at registration: window bits of the G table and
- * of the key tables (16 / 12 / 8; keys get the widest whose tables fit the
- * budget PBFTV_TABLE_BUDGET_MB, default min(16 GiB, free HBM / 4)), and the
- * HBM bytes the tables occupy per device. */
+/* Comb-table geometry chosen at registration: window bits of the G table
+ * (24 when 4 x its 5.9 GB fit, else 16/20) and of the key tables (the widest
+ * of 24 / 22 / 20 / 16 / 12 / 8 whose tables fit the budget: free HBM minus a
+ * 64 GiB reserve and the G table, or PBFTV_TABLE_BUDGET_MB), and the HBM bytes
+ * the tables occupy per device.  PBFTV_GBITS / PBFTV_QBITS force a pair. */
 int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uint64_t* out_table_bytes);
 
 /* Verify n signatures: hashes (n*32), sig_rs (n*64: r||s big-endian),
