@@ -498,7 +498,11 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint
     int d = (int)sdig[0][t] + 1;
     issue_entry_lds(sent, t, entry_ptr<WG>(gtab, 0, d));
 #pragma unroll 1
+#ifdef PBFTV_EXP_NOLOOP  // timing experiment only: prologue + epilogue without the comb (results wrong)
+    for (int j = 0; j < 1; ++j) {
+#else
     for (int j = 0; j < S::nD; ++j) {
+#endif
       uint32_t w16[16];
       read_entry_lds(sent, t, w16);
       const int dc = d;
