@@ -1,0 +1,97 @@
+/* openssl_standin.c -- CPU BASELINE / CROSS-CHECK ONLY (never part of the product).
+ *
+ * "a C++ std::thread x nproc OpenSSL libcrypto baseline
+ * (ECDSA_do_verify), labelled OpenSSL stand-in".  The reference's own verify
+ * path would be Go crypto/ecdsa, which cannot run here (no Go toolchain); this
+ * is the closest native CPU implementation in the image: OpenSSL 3 libcrypto's
+ * P-256 (nistz256 assembly on x86-64) timed on host threads, each thread with
+ * its own EC_KEY objects.  bench.py times it beside the GPU on the same
+ * signatures and checks that the accept bits agree.
+ *
+ * Semantics match Go crypto/ecdsa.Verify for 32-byte hashes: r, s outside
+ * [1, n-1] are rejected by OpenSSL; keys that OpenSSL refuses to load
+ * (off-curve, coordinate >= p) reject every signature naming them.
+ */
+#include <openssl/bn.h>
+#include <openssl/ec.h>
+#include <openssl/ecdsa.h>
+#include <openssl/err.h>
+#include <openssl/obj_mac.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+  const uint8_t* hashes;
+  const uint8_t* sigs;
+  const uint32_t* kidx;
+  uint64_t lo, hi;
+  const uint8_t* keys;
+  uint32_t nkeys;
+  uint8_t* ok;
+} job_t;
+
+static EC_KEY* load_key(const uint8_t xy[64]) {
+  EC_KEY* k = EC_KEY_new_by_curve_name(NID_X9_62_prime256v1);
+  BIGNUM* x = BN_bin2bn(xy, 32, NULL);
+  BIGNUM* y = BN_bin2bn(xy + 32, 32, NULL);
+  const int good = k && x && y && EC_KEY_set_public_key_affine_coordinates(k, x, y) == 1;
+  BN_free(x);
+  BN_free(y);
+  if (!good) {
+    EC_KEY_free(k);
+    ERR_clear_error();
+    return NULL;
+  }
+  return k;
+}
+
+static void* worker(void* arg) {
+  job_t* j = (job_t*)arg;
+  EC_KEY** ks = (EC_KEY**)calloc(j->nkeys ? j->nkeys : 1, sizeof(EC_KEY*));
+  for (uint32_t k = 0; k < j->nkeys; ++k) ks[k] = load_key(j->keys + 64ull * k);
+  for (uint64_t i = j->lo; i < j->hi; ++i) {
+    const uint32_t k = j->kidx[i];
+    uint8_t ok = 0;
+    if (k < j->nkeys && ks[k]) {
+      ECDSA_SIG* s = ECDSA_SIG_new();
+      BIGNUM* r = BN_bin2bn(j->sigs + 64 * i, 32, NULL);
+      BIGNUM* ss = BN_bin2bn(j->sigs + 64 * i + 32, 32, NULL);
+      ECDSA_SIG_set0(s, r, ss);
+      ok = ECDSA_do_verify(j->hashes + 32 * i, 32, s, ks[k]) == 1;
+      ECDSA_SIG_free(s);
+      ERR_clear_error();
+    }
+    j->ok[i] = ok;
+  }
+  for (uint32_t k = 0; k < j->nkeys; ++k) EC_KEY_free(ks[k]);
+  free(ks);
+  return NULL;
+}
+
+/* Verify n signatures on `threads` host threads; out_bitmap LSB-first,
+ * ceil(n/8) bytes.  Returns the number accepted, or -1 on allocation failure. */
+int64_t standin_ecdsa_p256_verify_batch(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* kidx, uint64_t n,
+                                        const uint8_t* keys, uint32_t nkeys, uint8_t* out_bitmap, int threads) {
+  if (threads < 1) threads = 1;
+  uint8_t* ok = (uint8_t*)calloc(n ? n : 1, 1);
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  job_t* jobs = (job_t*)calloc((size_t)threads, sizeof(job_t));
+  if (!ok || !th || !jobs) return -1;
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (job_t){hashes, sigs, kidx, n * t / threads, n * (t + 1) / threads, keys, nkeys, ok};
+    pthread_create(&th[t], NULL, worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  int64_t acc = 0;
+  memset(out_bitmap, 0, (n + 7) / 8);
+  for (uint64_t i = 0; i < n; ++i) {
+    out_bitmap[i >> 3] |= (uint8_t)(ok[i] << (i & 7));
+    acc += ok[i];
+  }
+  free(ok);
+  free(th);
+  free(jobs);
+  return acc;
+}

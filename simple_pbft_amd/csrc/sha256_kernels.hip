@@ -52,7 +52,19 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-__device__ __forceinline__ uint32_t load_word(const uint32_t* q, uint64_t j) { return q[j]; }
+// 16 dwords of one 64-B block from a 4-B aligned address as four 16-B loads
+// (global_load_dwordx4 needs only dword alignment): a quarter of the memory
+// instructions -- and of the 64-lane cache-line fan-out -- of dword loads.
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ void load_block16(const uint32_t* __restrict__ q, uint32_t d[16]) {
+  const u32x4_a4* v = reinterpret_cast<const u32x4_a4*>(q);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const u32x4_a4 x = v[k];
+    d[4 * k] = x.x; d[4 * k + 1] = x.y; d[4 * k + 2] = x.z; d[4 * k + 3] = x.w;
+  }
+}
 
 __global__ void __launch_bounds__(256) k_sha256(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
                                                 const uint32_t* __restrict__ lengths,
@@ -62,27 +74,33 @@ __global__ void __launch_bounds__(256) k_sha256(const uint8_t* __restrict__ data
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t m = order ? order[i] : i;
-  const uintptr_t a = (uintptr_t)(data + offsets[m]);
+  const uint8_t* base = data + offsets[m];  // pointer arithmetic (not an int round trip) keeps global loads
   const uint32_t len = lengths[m];
-  const uint32_t sh = (uint32_t)(a & 3u);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a - sh);
+  const uint32_t sh = (uint32_t)((uintptr_t)base & 3u);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(base - sh);
   uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
   const uint32_t nfull = len >> 6;
   uint32_t w[16];
+  // block b's 17 dwords (the 17th only for a misaligned message) are loaded
+  // while block b - 1 is compressed
+  uint32_t d[17];
+  if (nfull) {
+    load_block16(q, d);
+    d[16] = sh ? q[16] : 0u;
+  }
   for (uint32_t blk = 0; blk < nfull; ++blk) {
-    const uint32_t* qb = q + 16ull * blk;
-    uint32_t d[17];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) d[j] = qb[j];
-    d[16] = sh ? qb[16] : 0u;
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[j + 1], d[j], sh));
+    if (blk + 1 < nfull) {
+      const uint32_t* qb = q + 16ull * (blk + 1);
+      load_block16(qb, d);
+      d[16] = sh ? qb[16] : 0u;
+    }
     compress(st, w);
   }
   // tail: rem bytes (0..63) + 0x80 + zeros + 64-bit bit length, in one or two blocks
   const uint32_t rem = len - (nfull << 6);
   const uint32_t* qt = q + 16ull * nfull;
-  uint32_t d[17];
 #pragma unroll
   for (int j = 0; j < 17; ++j) d[j] = (4u * j < rem + sh) ? qt[j] : 0u;
 #pragma unroll

@@ -7,11 +7,13 @@ every committed ECDSA vector."""
 from __future__ import annotations
 
 import hashlib
+import os
+import subprocess
 
 import numpy as np
 import pytest
 
-from conftest import fixture_arrays
+from conftest import ROOT, fixture_arrays
 from oracle import gojson, openssl_xcheck, p256
 
 
@@ -159,3 +161,24 @@ def test_oracle_sign_roundtrip(oracle_lib):
                                        int.from_bytes(sig[32:].tobytes(), "big"),
                                        int.from_bytes(pub[:32].tobytes(), "big"),
                                        int.from_bytes(pub[32:].tobytes(), "big"))
+
+
+def test_openssl_standin_threads_match_fixtures(ecdsa_fixtures):
+    """The multi-threaded OpenSSL stand-in CPU baseline (oracle/openssl_standin.c,
+    bench.py's cpu_openssl_standin) gives the golden accept bits at 1 and 4 threads."""
+    import ctypes
+    so = os.path.join(ROOT, "oracle", "libopenssl_standin.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True)
+    L = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    L.standin_ecdsa_p256_verify_batch.restype = ctypes.c_int64
+    L.standin_ecdsa_p256_verify_batch.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_int]
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    n = len(kidx)
+    for threads in (1, 4):
+        bm = np.zeros((n + 7) // 8, np.uint8)
+        acc = L.standin_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n,
+                                                keys.ctypes.data, len(keys), bm.ctypes.data, threads)
+        got = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+        assert (got == expect).all() and acc == expect.sum()
