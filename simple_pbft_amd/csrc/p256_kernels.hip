@@ -636,7 +636,7 @@ __device__ __forceinline__ void wave_sum_lanes(jac& P, bool& inf, const uint32_t
 // Each step every lane of the quad does ONE field multiplication on operands
 // picked by its role (lane & 3), and the products are broadcast inside the
 // quad with DPP quad_perm moves (plain VALU, no LDS).  A Jacobian addition
-// (12M + 4S serially) becomes 5 multiplication steps, the affine + affine
+// (add-2008-s: 12M + 2S) becomes 4 multiplication steps, the affine + affine
 // first level 3 steps.
 template <int K>
 __device__ __forceinline__ void quad_bcast(fe& d, const fe& s) {
@@ -669,76 +669,71 @@ __device__ __forceinline__ void quad_mul(fe& p, int role, const fe& a0, const fe
   fe_mul(p, a, b);
 }
 
-// (gx, gy) + (qx, qy), both affine (mmadd-2007-bl); exc if x-coordinates meet.
-__device__ __forceinline__ void quad_mmadd(jac& r, bool& exc, int role, const fe& gx, const fe& gy, const fe& qx,
-                                           const fe& qy) {
-  fe h, t, rr, p, hh, r2, i4, jj, v, x3, a, b;
-  fe_sub(h, qx, gx);
-  fe_sub(t, qy, gy);
-  fe_add(rr, t, t);                                   // r = 2 (Y2 - Y1), lazy
-  exc = fe_is_zero(h);
-  quad_mul(p, role, h, h, rr, rr, h, h, rr, rr);      // HH, r^2
-  quad_bcast<0>(hh, p);
-  quad_bcast<1>(r2, p);
-  fe_mul_small(t, hh, 2);
-  fe_add(i4, t, t);                                   // I = 4 HH (lazy)
-  quad_mul(p, role, h, i4, gx, i4, h, i4, gx, i4);    // J = H I, V = X1 I
-  quad_bcast<0>(jj, p);
-  quad_bcast<1>(v, p);
-  fe_sub(t, r2, jj);
-  fe_add(a, v, v);
-  fe_sub(x3, t, a);                                   // X3 = r^2 - J - 2V
-  fe_sub(t, v, x3);
-  quad_mul(p, role, rr, t, gy, jj, rr, t, gy, jj);    // r (V - X3), Y1 J
-  quad_bcast<0>(a, p);
-  quad_bcast<1>(b, p);
-  fe_add(t, b, b);
-  fe_sub(r.y, a, t);                                  // Y3 = r (V - X3) - 2 Y1 J
-  fe_mul_small(r.z, h, 2);                            // Z3 = 2 H
+// (gx, gy) + (qx, qy), both affine, into XYZZ (mmadd-2008-s, 3 steps); exc if
+// the x-coordinates meet.
+__device__ __forceinline__ void quad_mmadd_xyzz(xyzz& r, bool& exc, int role, const fe& gx, const fe& gy,
+                                                const fe& qx, const fe& qy) {
+  fe p, rr, pp, r2, ppp, qq, x3, t, a, b, prod;
+  fe_sub(p, qx, gx);
+  fe_sub(rr, qy, gy);
+  exc = fe_is_zero(p);
+  quad_mul(prod, role, p, p, rr, rr, p, p, rr, rr);          // PP, R^2
+  quad_bcast<0>(pp, prod);
+  quad_bcast<1>(r2, prod);
+  quad_mul(prod, role, p, pp, gx, pp, p, pp, gx, pp);        // PPP, Q = X1 PP
+  quad_bcast<0>(ppp, prod);
+  quad_bcast<1>(qq, prod);
+  fe_add(t, ppp, qq);
+  fe_add(t, t, qq);
+  fe_sub(x3, r2, t);                                         // X3 = R^2 - PPP - 2Q
+  fe_sub(t, qq, x3);
+  quad_mul(prod, role, rr, t, gy, ppp, rr, t, gy, ppp);      // R (Q - X3), Y1 PPP
+  quad_bcast<0>(a, prod);
+  quad_bcast<1>(b, prod);
+  fe_sub(r.y, a, b);
   r.x = x3;
+  r.zz = pp;
+  r.zzz = ppp;
 }
 
-// r = p + q (both finite Jacobian), the jac_add formulas in 5 steps; exc if H == 0.
-__device__ __forceinline__ void quad_jadd(jac& r, bool& exc, int role, const jac& P, const jac& Q) {
-  fe p, z1z1, z2z2, z1z2, u1, u2, t1, t2, h, s1, s2, hh, z3, rr, hhh, v, r2, x3, t, a, b;
-  quad_mul(p, role, P.z, P.z, Q.z, Q.z, P.z, Q.z, P.z, Q.z);
-  quad_bcast<0>(z1z1, p);
-  quad_bcast<1>(z2z2, p);
-  quad_bcast<2>(z1z2, p);
-  quad_mul(p, role, P.x, z2z2, Q.x, z1z1, Q.z, z2z2, P.z, z1z1);
-  quad_bcast<0>(u1, p);
-  quad_bcast<1>(u2, p);
-  quad_bcast<2>(t1, p);
-  quad_bcast<3>(t2, p);
-  fe_sub(h, u2, u1);
-  exc = fe_is_zero(h);
-  quad_mul(p, role, P.y, t1, Q.y, t2, h, h, z1z2, h);
-  quad_bcast<0>(s1, p);
-  quad_bcast<1>(s2, p);
-  quad_bcast<2>(hh, p);
-  quad_bcast<3>(z3, p);
+// r = P + Q (both finite XYZZ), add-2008-s in 4 steps of <= 4 products (the
+// Jacobian quad_jadd needs 5); exc if the x-coordinates meet (P == 0).
+__device__ __forceinline__ void quad_xyzz_add(xyzz& r, bool& exc, int role, const xyzz& P, const xyzz& Q) {
+  fe prod, u1, u2, s1, s2, p, rr, pp, r2, zz12, zzz12, ppp, qq, x3, t, a, b;
+  quad_mul(prod, role, P.x, Q.zz, Q.x, P.zz, P.y, Q.zzz, Q.y, P.zzz);      // U1, U2, S1, S2
+  quad_bcast<0>(u1, prod);
+  quad_bcast<1>(u2, prod);
+  quad_bcast<2>(s1, prod);
+  quad_bcast<3>(s2, prod);
+  fe_sub(p, u2, u1);
   fe_sub(rr, s2, s1);
-  quad_mul(p, role, hh, h, u1, hh, rr, rr, hh, h);
-  quad_bcast<0>(hhh, p);
-  quad_bcast<1>(v, p);
-  quad_bcast<2>(r2, p);
-  fe_sub(t, r2, hhh);
-  fe_add(a, v, v);
-  fe_sub(x3, t, a);                                   // X3 = r^2 - H^3 - 2 U1 H^2
-  fe_sub(t, v, x3);
-  quad_mul(p, role, rr, t, s1, hhh, rr, t, s1, hhh);
-  quad_bcast<0>(a, p);
-  quad_bcast<1>(b, p);
-  fe_sub(r.y, a, b);                                  // Y3 = r (V - X3) - S1 H^3
+  exc = fe_is_zero(p);
+  quad_mul(prod, role, p, p, rr, rr, P.zz, Q.zz, P.zzz, Q.zzz);             // PP, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2
+  quad_bcast<0>(pp, prod);
+  quad_bcast<1>(r2, prod);
+  quad_bcast<2>(zz12, prod);
+  quad_bcast<3>(zzz12, prod);
+  quad_mul(prod, role, p, pp, u1, pp, zz12, pp, zz12, pp);                  // PPP, Q = U1 PP, ZZ3
+  quad_bcast<0>(ppp, prod);
+  quad_bcast<1>(qq, prod);
+  quad_bcast<2>(r.zz, prod);
+  fe_add(t, ppp, qq);
+  fe_add(t, t, qq);
+  fe_sub(x3, r2, t);                                                        // X3 = R^2 - PPP - 2Q
+  fe_sub(t, qq, x3);
+  quad_mul(prod, role, rr, t, s1, ppp, zzz12, ppp, zzz12, ppp);             // R (Q - X3), S1 PPP, ZZZ3
+  quad_bcast<0>(a, prod);
+  quad_bcast<1>(b, prod);
+  quad_bcast<2>(r.zzz, prod);
+  fe_sub(r.y, a, b);                                                        // Y3 = R (Q - X3) - S1 PPP
   r.x = x3;
-  r.z = z3;                                           // Z3 = Z1 Z2 H
 }
 
 // quad q = window q: G entry + Q entry, then a butterfly over the quads.
 // exc reports a doubling / cancellation anywhere (the caller reruns the
 // signature with wave_sum_lanes).
 template <int WG, int WQ>
-__device__ __forceinline__ void wave_sum_quads(jac& P, bool& inf, bool& exc, const uint32_t u1[8],
+__device__ __forceinline__ void wave_sum_quads(xyzz& P, bool& inf, bool& exc, const uint32_t u1[8],
                                                const uint32_t u2[8], const uint4* __restrict__ gtab,
                                                const uint4* __restrict__ qtab) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
@@ -771,9 +766,9 @@ __device__ __forceinline__ void wave_sum_quads(jac& P, bool& inf, bool& exc, con
     fe_neg_lazy(ny, qy);
     fe_norm(qy, ny);
   }
-  jac S;
+  xyzz S;
   bool e0;
-  quad_mmadd(S, e0, role, gx, gy, qx, qy);            // every quad runs it; selected below
+  quad_mmadd_xyzz(S, e0, role, gx, gy, qx, qy);       // every quad runs it; selected below
   exc = d1 != 0 && d2 != 0 && e0;
   inf = d1 == 0 && d2 == 0;
   const bool both = d1 != 0 && d2 != 0, g_only = d1 != 0;
@@ -781,22 +776,46 @@ __device__ __forceinline__ void wave_sum_quads(jac& P, bool& inf, bool& exc, con
   fe_set(one, kOneP);
   fe_sel3(P.x, both, S.x, g_only, gx, qx);
   fe_sel3(P.y, both, S.y, g_only, gy, qy);
-  fe_sel3(P.z, both, S.z, true, one, one);
+  fe_sel3(P.zz, both, S.zz, true, one, one);
+  fe_sel3(P.zzz, both, S.zzz, true, one, one);
 #pragma unroll 1
   for (int m = 1; m < nW; m <<= 1) {
-    jac Q;
+    xyzz Q;
     shfl_xor_fe(Q.x, P.x, 4 * m);
     shfl_xor_fe(Q.y, P.y, 4 * m);
-    shfl_xor_fe(Q.z, P.z, 4 * m);
+    shfl_xor_fe(Q.zz, P.zz, 4 * m);
+    shfl_xor_fe(Q.zzz, P.zzz, 4 * m);
     const bool qinf = __shfl_xor((int)inf, 4 * m, 64) != 0;
     bool e;
-    quad_jadd(S, e, role, P, Q);
+    quad_xyzz_add(S, e, role, P, Q);
     exc = exc || (e && !inf && !qinf);
     fe_sel3(P.x, inf, Q.x, qinf, P.x, S.x);
     fe_sel3(P.y, inf, Q.y, qinf, P.y, S.y);
-    fe_sel3(P.z, inf, Q.z, qinf, P.z, S.z);
+    fe_sel3(P.zz, inf, Q.zz, qinf, P.zz, S.zz);
+    fe_sel3(P.zzz, inf, Q.zzz, qinf, P.zzz, S.zzz);
     inf = inf && qinf;
   }
+}
+
+// ecdsa_scalars with the inversion fed the plain s (no Montgomery round trip
+// in front of it): w = s^-1 -> w R -> u1 = e w, u2 = r w (two independent
+// products) -- one dependent Montgomery product fewer on the latency path.
+__device__ __forceinline__ void ecdsa_scalars_plain_inv(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
+                                                        uint32_t u1[8], uint32_t u2[8]) {
+  uint32_t iw[8];
+  inv_mod_n_words(iw, s);  // 0 < s < n checked by sig_ok
+  fe inv, r2n, w, ev, rv, t1, t2;
+  fe_from_words(inv, iw);
+  fe_set(r2n, kR2N);
+  fn_mul(w, inv, r2n);     // s^-1 R
+  fe_from_words(ev, e);
+  fe_from_words(rv, r);
+  fn_mul(t1, ev, w);       // e s^-1 (e < 2^256 < 2n)
+  fn_mul(t2, rv, w);
+  fn_canon(t1, t1);
+  fn_canon(t2, t2);
+  fe_to_words(u1, t1);
+  fe_to_words(u2, t2);
 }
 
 template <int WG, int WQ>
@@ -816,18 +835,21 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
   if (sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s)) {  // wave-uniform branch
     uint32_t e[8], u1[8], u2[8];
     load_be256(hashes + 32 * i, e);
-    ecdsa_scalars(e, r, s, u1, u2);
+    ecdsa_scalars_plain_inv(e, r, s, u1, u2);
     const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
-    jac P;
     bool inf;
+    bool exc = true;
     if constexpr (nW <= 16) {
-      bool exc;
+      xyzz P;
       wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
-      if (__any(exc)) wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qtab);  // doubling somewhere: exact rerun
-    } else {
-      wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qtab);
+      exc = __any(exc);
+      if (!exc) ok = ecdsa_check(P, !inf, r);
     }
-    ok = ecdsa_check(P, !inf, r);
+    if (exc) {  // windows outnumber the quads, or a doubling somewhere: exact lane-per-window rerun
+      jac P;
+      wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qtab);
+      ok = ecdsa_check(P, !inf, r);
+    }
   }
   if (j != 0) return;
   if (okbytes) {

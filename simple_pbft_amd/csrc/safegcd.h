@@ -73,6 +73,36 @@ PBFTV_HD int32_t divsteps30_var(int32_t eta, uint32_t f, uint32_t g, trans30& t)
   return eta;
 }
 
+// 30 divsteps in constant time (branch-free masks; Bernstein-Yang with
+// zeta = -(delta + 1/2), as libsecp256k1's modinv32 divsteps_30): a straight
+// dependent chain with no data-dependent branches -- for the latency path,
+// where one wave runs one inversion and divergence-free straight-line code
+// lets the compiler overlap it with the previous batch's matrix update.
+PBFTV_HD int32_t divsteps30_ct(int32_t zeta, uint32_t f, uint32_t g, trans30& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  PBFTV_UNROLL for (int i = 0; i < 30; ++i) {
+    uint32_t c1 = (uint32_t)(zeta >> 31);  // zeta < 0
+    const uint32_t c2 = 0u - (g & 1u);     // g odd
+    const uint32_t x = (f ^ c1) - c1, y = (u ^ c1) - c1, z = (v ^ c1) - c1;
+    g += x & c2;
+    q += y & c2;
+    r += z & c2;
+    c1 &= c2;
+    zeta = (int32_t)(((uint32_t)zeta ^ c1) - 1u);
+    f += g & c1;
+    u += q & c1;
+    v += r & c1;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return zeta;
+}
+
 // (f, g) <- t (f, g) / 2^30 (exact)
 PBFTV_HD void update_fg30(s30& f, s30& g, const trans30& t) {
   int64_t cf = (int64_t)t.u * f.v[0] + (int64_t)t.v * g.v[0];
@@ -197,6 +227,30 @@ PBFTV_HD void inv_mod_n_words(uint32_t out[8], const uint32_t x[8]) {
   }
   // f = +-1; d in (-2n, n)
   if (f.v[8] < 0) s30_neg(d);  // now in (-n, 2n)
+  if (d.v[8] < 0) s30_add_n(d, 1);
+  if (d.v[8] < 0) s30_add_n(d, 1);
+  if (s30_ge_n(d)) s30_add_n(d, -1);
+  s30_to_words(out, d);
+}
+
+// inv_mod_n_words with constant-time divsteps (all 25 batches; same result).
+PBFTV_HD void inv_mod_n_words_ct(uint32_t out[8], const uint32_t x[8]) {
+  s30 f, g, d, e;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    f.v[i] = (int32_t)kN30[i];
+    d.v[i] = 0;
+    e.v[i] = 0;
+  }
+  e.v[0] = 1;
+  words_to_s30(g, x);
+  int32_t zeta = -1;
+  for (int it = 0; it < 25; ++it) {
+    trans30 t;
+    zeta = divsteps30_ct(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    update_de30(d, e, t);
+    update_fg30(f, g, t);
+  }
+  if (f.v[8] < 0) s30_neg(d);
   if (d.v[8] < 0) s30_add_n(d, 1);
   if (d.v[8] < 0) s30_add_n(d, 1);
   if (s30_ge_n(d)) s30_add_n(d, -1);

@@ -63,6 +63,7 @@ void h_fe_to_words(const uint32_t* a, uint32_t* w) {
   fe_to_words(w, x);
 }
 void h_inv_n_words(const uint32_t* x, uint32_t* out) { inv_mod_n_words(out, x); }
+void h_inv_n_words_ct(const uint32_t* x, uint32_t* out) { inv_mod_n_words_ct(out, x); }
 
 void h_fn_inv_mont(const uint32_t* a, int use_gcd, uint32_t* r) {
   fe x, y;

@@ -10,7 +10,7 @@
 
 using namespace pbftv;
 
-constexpr int kStages = 9;
+constexpr int kStages = 11;
 
 __global__ void probe(const uint32_t* in, uint64_t* ticks, uint32_t* sink, int reps, uint32_t lane_mask) {
   uint32_t e[8], r[8], s[8];
@@ -80,6 +80,22 @@ __global__ void probe(const uint32_t* in, uint64_t* ticks, uint32_t* sink, int r
     acc += w[2];
   }
   t[9] = wall_clock64();
+  for (int k = 0; k < reps; ++k) {  // 9: constant-time divsteps, VALU operands
+    uint32_t w[8], sv[8];
+    for (int q = 0; q < 8; ++q) sv[q] = s[q] ^ (threadIdx.x & lane_mask);
+    sv[1] ^= k;
+    inv_mod_n_words_ct(w, sv);
+    acc += w[2];
+  }
+  t[10] = wall_clock64();
+  for (int k = 0; k < reps; ++k) {  // 10: constant-time divsteps, SALU operands
+    uint32_t w[8], sv[8];
+    for (int q = 0; q < 8; ++q) sv[q] = __builtin_amdgcn_readfirstlane(s[q] ^ (threadIdx.x & lane_mask));
+    sv[1] ^= k;
+    inv_mod_n_words_ct(w, sv);
+    acc += w[2];
+  }
+  t[11] = wall_clock64();
   if (threadIdx.x == 0) {
     for (int i = 0; i < kStages; ++i) ticks[i] = t[i + 1] - t[i];
   }
@@ -108,9 +124,9 @@ int main() {
   hipMemcpy(t, d_t, sizeof(t), hipMemcpyDeviceToHost);
   const char* names[kStages] = {"ecdsa_scalars (safegcd)", "inv_mod_n safegcd", "fn_inv_mont Fermat",
                                 "fe_mul", "jac_add", "jac_madd<true>", "jac_double", "inv_mod_n VALU operands",
-                                "inv_mod_n SALU operands"};
+                                "inv_mod_n SALU operands", "inv ct VALU", "inv ct SALU"};
   const double per[kStages] = {1.0 * reps, 1.0 * reps, 1.0 * reps, 100.0 * reps, 1.0 * reps, 1.0 * reps, 1.0 * reps,
-                                1.0 * reps, 1.0 * reps};
+                                1.0 * reps, 1.0 * reps, 1.0 * reps, 1.0 * reps};
   printf("{\"wall_clock_khz\": %d", rate_khz);
   for (int i = 0; i < kStages; ++i) printf(", \"%s_us\": %.3f", names[i], t[i] / per[i] * 1e3 / rate_khz);
   printf("}\n");
