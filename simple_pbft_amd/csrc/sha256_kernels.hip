@@ -15,6 +15,10 @@
 
 namespace pbftv {
 
+#ifndef PBFTV_SHA_WAVES
+#define PBFTV_SHA_WAVES 1  // min waves per SIMD for k_sha256
+#endif
+
 __device__ __constant__ static const uint32_t kK256[64] = {
     0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
     0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
@@ -26,6 +30,11 @@ __device__ __constant__ static const uint32_t kK256[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// three-way XOR as ONE v_bitop3_b32 (truth table 0x96); the compiler leaves
+// a ^ b ^ c as two v_xor_b32 (~220 extra instructions per block)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
@@ -36,15 +45,15 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
       wr = w[r];
     } else {
       const uint32_t x = w[(r + 1) & 15], y = w[(r + 14) & 15];
-      const uint32_t s0 = rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3);
-      const uint32_t s1 = rotr(y, 17) ^ rotr(y, 19) ^ (y >> 10);
+      const uint32_t s0 = xor3(rotr(x, 7), rotr(x, 18), x >> 3);
+      const uint32_t s1 = xor3(rotr(y, 17), rotr(y, 19), y >> 10);
       w[r & 15] += s0 + w[(r + 9) & 15] + s1;
       wr = w[r & 15];
     }
-    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = h + S1 + ch + kK256[r] + wr;
-    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
     const uint32_t mj = (a & b) | (c & (a | b));
     const uint32_t t2 = S0 + mj;
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
@@ -66,7 +75,7 @@ __device__ __forceinline__ void load_block16(const uint32_t* __restrict__ q, uin
   }
 }
 
-__global__ void __launch_bounds__(256) k_sha256(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
+__global__ void __launch_bounds__(256, PBFTV_SHA_WAVES) k_sha256(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
                                                 const uint32_t* __restrict__ lengths,
                                                 const uint32_t* __restrict__ order, uint64_t n,
                                                 uint8_t* __restrict__ digests, const uint8_t* __restrict__ expected,
