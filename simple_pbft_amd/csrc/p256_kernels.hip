@@ -25,7 +25,7 @@
 namespace pbftv {
 
 #ifndef PBFTV_COMB_WAVES
-#define PBFTV_COMB_WAVES 2  // min waves per SIMD for k_ecdsa_comb (register budget 512 / this)
+#define PBFTV_COMB_WAVES 4  // min waves per SIMD for k_ecdsa_comb: 128 VGPRs; +1.2 % over 2 (tools/ab.sh)
 #endif
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
