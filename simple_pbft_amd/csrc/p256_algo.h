@@ -29,10 +29,10 @@ namespace pbftv {
 // |d| * 2^(W i) * B as affine (x, y), canonical Montgomery-form, 8+8 LE words.
 template <int W>
 struct CombGeom {
-  static_assert(W >= 8 && W <= 24, "window width");
+  static_assert(W >= 8 && W <= 26, "window width");
   static_assert(256 % W <= W - 2, "top window must absorb the recoding carry");
   static constexpr int kW = W;
-  static constexpr int kWin = 256 / W + 1;  // 33 (W=8), 22 (12), 17 (16), 13 (20), 11 (24)
+  static constexpr int kWin = 256 / W + 1;  // 33 (W=8), 22 (12), 17 (16), 13 (20), 12 (22), 11 (24), 10 (26)
   static constexpr int kEnt = 1 << (W - 1);
   static constexpr uint64_t kWords = (uint64_t)kWin * kEnt * 16;
   static constexpr uint64_t kBytes = kWords * 4;

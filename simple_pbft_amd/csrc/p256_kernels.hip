@@ -47,7 +47,8 @@ struct TabGeom {
   using G = CombGeom<W>;
   // L table: (lo+1) B_i, lo < CL; H table: hi (CL B_i), 1 <= hi < NH.  Up to
   // W = 16 CL = 256; wider windows split E = CL * NH near sqrt(E) so neither
-  // phase-2 walk gets long (W = 20: 1024 x 512, W = 24: 4096 x 2048).
+  // phase-2 walk gets long (W = 20: 1024 x 512, W = 24: 4096 x 2048,
+  // W = 26: 8192 x 4096).
   static constexpr int CL = G::kEnt < 256 ? G::kEnt : (W <= 16 ? 256 : 1 << (W / 2));
   static constexpr int NH = G::kEnt / CL;
   static constexpr int PC = CL < 64 ? CL : 64;              // entries per phase-3 lane
@@ -183,6 +184,7 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
     case 16: fill(CombGeom<16>()); break;
     case 20: fill(CombGeom<20>()); break;
     case 22: fill(CombGeom<22>()); break;
+    case 26: fill(CombGeom<26>()); break;
     default: fill(CombGeom<24>()); break;
   }
   return z;
@@ -196,6 +198,7 @@ size_t table_bytes(int w) {
     case 20: return CombGeom<20>::kBytes;
     case 22: return CombGeom<22>::kBytes;
     case 24: return CombGeom<24>::kBytes;
+    case 26: return CombGeom<26>::kBytes;
     default: return 0;
   }
 }
@@ -209,6 +212,7 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
     case 20: return build_tables_w<20>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     case 22: return build_tables_w<22>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     case 24: return build_tables_w<24>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    case 26: return build_tables_w<26>(keys_le, key0, nb, with_g, valid, tables, sc, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -881,7 +885,11 @@ hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_
   if (n == 0) return hipSuccess;
   if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
 #define PBFTV_WAVE(G, Q) launch_wave_w<G, Q>(hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes, st)
-  if (wg == 24 && wq == 22) PBFTV_WAVE(24, 22);
+  if (wg == 26 && wq == 22) PBFTV_WAVE(26, 22);
+  else if (wg == 26 && wq == 24) PBFTV_WAVE(26, 24);
+  else if (wg == 26 && wq == 20) PBFTV_WAVE(26, 20);
+  else if (wg == 26 && wq == 16) PBFTV_WAVE(26, 16);
+  else if (wg == 24 && wq == 22) PBFTV_WAVE(24, 22);
   else if (wg == 24 && wq == 24) PBFTV_WAVE(24, 24);
   else if (wg == 24 && wq == 20) PBFTV_WAVE(24, 20);
   else if (wg == 20 && wq == 20) PBFTV_WAVE(20, 20);
@@ -957,7 +965,11 @@ hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* fl
                              const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
                              uint8_t* bitmap, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (wg == 24 && wq == 22) launch_comb_w<24, 22>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  if (wg == 26 && wq == 22) launch_comb_w<26, 22>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 26 && wq == 24) launch_comb_w<26, 24>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 26 && wq == 20) launch_comb_w<26, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 26 && wq == 16) launch_comb_w<26, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
+  else if (wg == 24 && wq == 22) launch_comb_w<24, 22>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 24 && wq == 24) launch_comb_w<24, 24>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 24 && wq == 20) launch_comb_w<24, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
   else if (wg == 20 && wq == 20) launch_comb_w<20, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);

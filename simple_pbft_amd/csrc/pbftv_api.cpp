@@ -1,7 +1,7 @@
 // pbftv_api.cpp -- the C ABI of include/pbftv.h on top of the gfx950 kernels.
 //
 // One pbftv_ctx owns, per GPU: a non-blocking HIP stream, the comb tables of
-// G and every registered key (resident in HBM: ~264 KiB per key), and
+// G and every registered key (resident in HBM; see choose_bits), and
 // grow-only scratch.  Host-buffer batches are cut into contiguous shards
 // (multiples of 512 items, so every shard's bitmap starts on a byte and every
 // wave on a 64-item boundary), one per device, each driven by its own host
@@ -377,14 +377,14 @@ static int env_bits(const char* name, int dflt) {
   const char* e = getenv(name);
   if (!e) return dflt;
   const int v = atoi(e);
-  return (v == 8 || v == 12 || v == 16 || v == 20 || v == 22 || v == 24) ? v : dflt;
+  return (v == 8 || v == 12 || v == 16 || v == 20 || v == 22 || v == 24 || v == 26) ? v : dflt;
 }
 
 // Comb widths (G, keys) with instantiated kernels; the widest that fit win
 // (fewer windows = fewer mixed additions per verify).
 static bool combo_ok(int wg, int wq) {
-  static const int kCombos[][2] = {{24, 24}, {24, 22}, {24, 20}, {20, 20}, {24, 16},
-                                   {16, 16}, {16, 12}, {16, 8},  {8, 8}};
+  static const int kCombos[][2] = {{26, 24}, {26, 22}, {26, 20}, {26, 16}, {24, 24}, {24, 22}, {24, 20},
+                                   {20, 20}, {24, 16}, {16, 16}, {16, 12}, {16, 8},  {8, 8}};
   for (auto& c : kCombos)
     if (c[0] == wg && c[1] == wq) return true;
   return false;
@@ -393,35 +393,45 @@ static bool combo_ok(int wg, int wq) {
 // HBM kept free for batch buffers and other users of the device.
 constexpr size_t kTableReserve = 64ull << 30;
 
-// Key tables may take all of the device's free HBM but kTableReserve and the
-// 24-bit G table (an MI355X has 288 GB: 4 keys at 24-bit windows = 23.6 GB,
-// 100 keys at 22-bit = 161 GB, 1000 keys at 16-bit = 35 GB);
-// PBFTV_TABLE_BUDGET_MB, PBFTV_GBITS and PBFTV_QBITS override.
+// Table geometry: the pair (G, keys) with the fewest windows in total whose
+// tables fit the device's free HBM minus kTableReserve (an MI355X has 288 GB:
+// G at 26-bit windows = 21.5 GB; 4 keys at 24-bit = 23.6 GB; 100 keys at
+// 22-bit = 161 GB; 1000 keys at 16-bit = 35 GB).  Among equal totals the
+// narrower G wins (less HBM).  PBFTV_TABLE_BUDGET_MB caps the key tables;
+// PBFTV_GBITS / PBFTV_QBITS force a width.
 static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
-  const size_t g24 = pbftv::table_bytes(24);
-  size_t budget = free_bytes > kTableReserve + g24 ? free_bytes - kTableReserve - g24 : 0;
-  budget = std::max(budget, free_bytes / 8);
-  if (const char* e = getenv("PBFTV_TABLE_BUDGET_MB")) budget = (size_t)atoll(e) << 20;
   const uint64_t kk = k ? k : 1;
-  int q = 8;
-  for (int w : {24, 22, 20, 16, 12}) {
-    if (kk * pbftv::table_bytes(w) <= budget) {
-      q = w;
-      break;
+  const char* env_budget = getenv("PBFTV_TABLE_BUDGET_MB");
+  const int force_g = env_bits("PBFTV_GBITS", 0), force_q = env_bits("PBFTV_QBITS", 0);
+  auto windows = [](int w) { return 256 / w + 1; };
+  int best_g = 0, best_q = 0, best_win = 1 << 30;
+  for (int g : {16, 20, 24, 26}) {
+    if (force_g && g != force_g) continue;
+    const size_t gb = pbftv::table_bytes(g);
+    size_t budget = free_bytes > kTableReserve + gb ? free_bytes - kTableReserve - gb : 0;
+    if (g > 16 && budget == 0 && !force_g) continue;  // wide G tables only with room to spare
+    budget = std::max(budget, free_bytes / 8);
+    if (env_budget) budget = (size_t)atoll(env_budget) << 20;
+    for (int q : {24, 22, 20, 16, 12, 8}) {
+      if (force_q && q != force_q) continue;
+      if (!combo_ok(g, q)) continue;
+      if (!force_q && q > 8 && kk * pbftv::table_bytes(q) > budget) continue;
+      const int win = windows(g) + windows(q);
+      if (win < best_win) {
+        best_win = win;
+        best_g = g;
+        best_q = q;
+      }
+      break;  // widest fitting key width for this G
     }
   }
-  q = env_bits("PBFTV_QBITS", q);
-  const bool big_g = pbftv::table_bytes(24) * 4 <= free_bytes;
-  int g = env_bits("PBFTV_GBITS", (q >= 16 && big_g) ? 24 : 16);
-  if (!combo_ok(g, q)) {
-    if (q >= 22 && !big_g) q = 20;  // (20|24, 22|24) need the 24-bit G table
-    if (q >= 22) g = 24;
-    else if (q == 20) g = big_g ? 24 : 20;
-    else if (q == 16) g = (g == 24 && big_g) ? 24 : 16;
-    else if (!(g == 8 && q == 8)) g = 16;
+  if (!best_g) {  // forced pair without an instantiated kernel: nearest G for the key width
+    best_q = force_q ? force_q : 8;
+    best_g = best_q >= 20 ? 24 : (best_q == 8 && force_g == 8 ? 8 : 16);
+    if (!combo_ok(best_g, best_q)) best_g = 16;
   }
-  *wg = g;
-  *wq = q;
+  *wg = best_g;
+  *wq = best_q;
 }
 
 static int build_tables(Device& d, int w, const uint32_t* d_keys, uint32_t nb, int with_g, uint32_t* valid,

@@ -189,7 +189,8 @@ def test_ecdsa_random_vs_oracle(ver, oracle_lib, path):
     assert want.sum() > n // 2
 
 
-@pytest.mark.parametrize("gq", [(24, 24), (24, 22), (24, 20), (20, 20), (24, 16), (16, 16), (16, 12), (16, 8), (8, 8)])
+@pytest.mark.parametrize("gq", [(26, 24), (26, 22), (26, 20), (26, 16), (24, 24), (24, 22), (24, 20), (20, 20), (24, 16),
+                                (16, 16), (16, 12), (16, 8), (8, 8)])
 def test_ecdsa_every_table_width(oracle_lib, ecdsa_fixtures, gq, path, monkeypatch):
     """Golden vectors + random corruptions vs the oracle for every comb geometry."""
     from simple_pbft_amd import Verifier
@@ -303,7 +304,8 @@ def test_ecdsa_wave_path_edge_counts(ver, oracle_lib, monkeypatch):
         assert (got == want[:n]).all(), n
 
 
-@pytest.mark.parametrize("gq", [(24, 24), (24, 22), (24, 20), (20, 20), (24, 16), (16, 16), (16, 8), (8, 8)])
+@pytest.mark.parametrize("gq", [(26, 24), (26, 22), (24, 24), (24, 22), (24, 20), (20, 20), (24, 16), (16, 16), (16, 8),
+                                (8, 8)])
 def test_ecdsa_crafted_exceptional_sums(gq, path, monkeypatch):
     from simple_pbft_amd import Verifier
     monkeypatch.setenv("PBFTV_GBITS", str(gq[0]))
