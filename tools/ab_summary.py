@@ -15,7 +15,8 @@ for f in sorted(glob.glob(os.path.join(d, "*.json"))):
     except Exception:
         print(v, "FAILED", open(f).read()[-300:])
         continue
-    res[v].append((j["value"] / 1e6, j["kernels"]["ecdsa_comb"]["avg_ms"], j["kernels"]["ecdsa_scalars"]["avg_ms"], j["check"]))
+    res[v].append((j["value"] / 1e6, {k: x["avg_ms"] for k, x in j["kernels"].items()}, j["check"]))
 for v, rs in res.items():
-    print(f"{v:12s} Mverif/s {statistics.median(r[0] for r in rs):7.1f}  comb {statistics.median(r[1] for r in rs):.4f} ms"
-          f"  scalars {statistics.median(r[2] for r in rs):.4f} ms  checks {[r[3] for r in rs]}")
+    ks = {k: statistics.median(r[1][k] for r in rs) for k in rs[0][1]}
+    print(f"{v:12s} Mverif/s {statistics.median(r[0] for r in rs):7.1f}  " +
+          "  ".join(f"{k} {t:.4f} ms" for k, t in ks.items()) + f"  checks {[r[2] for r in rs]}")
