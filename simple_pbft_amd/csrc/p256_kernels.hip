@@ -835,10 +835,10 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
   const int j = threadIdx.x;
   const uint64_t i = blockIdx.x;
   bool ok = false;
-  uint32_t r[8], s[8];
+  uint32_t r[8], s[8], e[8];
+  load_be256(hashes + 32 * i, e);  // issued with sig_ok's loads: one round trip to the (host) inputs
   if (sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s)) {  // wave-uniform branch
-    uint32_t e[8], u1[8], u2[8];
-    load_be256(hashes + 32 * i, e);
+    uint32_t u1[8], u2[8];
     ecdsa_scalars_plain_inv(e, r, s, u1, u2);
     const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
     bool inf;

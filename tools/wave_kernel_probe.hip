@@ -1,0 +1,107 @@
+// wave_kernel_probe.hip -- stage timestamps of the one-wave-per-signature
+// latency kernel (k_ecdsa_wave's body, p256_kernels.hip, replicated with
+// wall_clock64() stamps): input loads, scalars (safegcd), quad comb, check.
+// Tables: 24-bit G and one 22-bit key table (Q = G), built with the product's
+// table kernels.  Measurement tool for DESIGN.md (not part of the product).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/wave_kernel_probe.hip -o tools/wave_kernel_probe
+#include "../simple_pbft_amd/csrc/p256_kernels.hip"
+
+#include <cstdio>
+#include <vector>
+
+using namespace pbftv;
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+constexpr int WG = 24, WQ = 22;
+
+__global__ void __launch_bounds__(64) probe(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
+                                            const uint32_t* key_valid, const uint4* gtab, const uint4* qtabs,
+                                            uint64_t* stamps, uint32_t* sink) {
+  const uint64_t i = blockIdx.x;
+  uint64_t t[6];
+  t[0] = wall_clock64();
+  uint32_t r[8], s[8], e[8];
+  load_be256(hashes + 32 * i, e);
+  const bool okin = sig_ok(sigs, key_idx, key_valid, 1, i, r, s);
+  uint32_t acc = okin;
+  for (int k = 0; k < 8; ++k) acc += e[k] ^ r[k] ^ s[k];
+  t[1] = wall_clock64();
+  uint32_t u1[8], u2[8];
+  ecdsa_scalars_plain_inv(e, r, s, u1, u2);
+  acc += u1[0] ^ u2[0];
+  t[2] = wall_clock64();
+  const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
+  xyzz P;
+  bool inf, exc;
+  wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
+  acc += P.x.v[0] ^ (uint32_t)exc;
+  t[3] = wall_clock64();
+  const bool ok = ecdsa_check(P, !inf, r);
+  acc += ok;
+  t[4] = wall_clock64();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 4; ++k) stamps[i * 4 + k] = t[k + 1] - t[k];
+    sink[i] = acc;
+  }
+}
+
+int main() {
+  const uint32_t n = 64;
+  // key = G (valid), random in-range r, s, e: the stages run in full whatever the verdict
+  std::vector<uint8_t> h(32 * n), sg(64 * n), key(64);
+  uint32_t x = 12345;
+  auto rnd = [&]() { x = x * 1664525u + 1013904223u; return (uint8_t)(x >> 24); };
+  for (auto& b : h) b = rnd();
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 64; ++k) sg[64 * i + k] = (k % 32 == 0) ? 0x7F : rnd();  // r, s < n
+  const uint32_t gx[8] = {0xd898c296, 0xf4a13945, 0x2deb33a0, 0x77037d81, 0x63a440f2, 0xf8bce6e5, 0xe12c4247, 0x6b17d1f2};
+  const uint32_t gy[8] = {0x37bf51f5, 0xcbb64068, 0x6b315ece, 0x2bce3357, 0x7c0f9e16, 0x8ee7eb4a, 0xfe1a7f9b, 0x4fe342e2};
+  std::vector<uint32_t> keys_le(16);
+  for (int k = 0; k < 8; ++k) { keys_le[k] = gx[k]; keys_le[8 + k] = gy[k]; }
+  uint8_t *dh, *ds;
+  uint32_t *dk, *dkeys, *dvalid, *dsink;
+  uint64_t* dst;
+  CHECK(hipMalloc(&dh, h.size()));
+  CHECK(hipMalloc(&ds, sg.size()));
+  CHECK(hipMalloc(&dk, 4 * n));
+  CHECK(hipMalloc(&dkeys, 64));
+  CHECK(hipMalloc(&dvalid, 64));
+  CHECK(hipMalloc(&dsink, 4 * n));
+  CHECK(hipMalloc(&dst, 8 * 4 * n));
+  CHECK(hipMemcpy(dh, h.data(), h.size(), hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(ds, sg.data(), sg.size(), hipMemcpyHostToDevice));
+  CHECK(hipMemset(dk, 0, 4 * n));
+  CHECK(hipMemcpy(dkeys, keys_le.data(), 64, hipMemcpyHostToDevice));
+  uint32_t *gt, *qt;
+  CHECK(hipMalloc(&gt, table_bytes(WG)));
+  CHECK(hipMalloc(&qt, table_bytes(WQ)));
+  for (int w : {WG, WQ}) {
+    const TableScratchSizes z = table_scratch_sizes(w, 1);
+    void *b, *l, *hb, *ss, *es;
+    CHECK(hipMalloc(&b, z.bases)); CHECK(hipMalloc(&l, z.lbuf)); CHECK(hipMalloc(&hb, z.hbuf));
+    CHECK(hipMalloc(&ss, z.small_scratch)); CHECK(hipMalloc(&es, z.entry_scratch));
+    TableScratch sc{b, l, hb, ss, es, z.entry_lanes};
+    CHECK(launch_build_tables(w, dkeys, 0, 1, w == WG ? 1 : 0, dvalid, w == WG ? gt : qt, sc, 0));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipFree(b)); CHECK(hipFree(l)); CHECK(hipFree(hb)); CHECK(hipFree(ss)); CHECK(hipFree(es));
+  }
+  int rate_khz = 0;
+  CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL(probe, dim3(rep == 2 ? n : 1), dim3(64), 0, 0, dh, ds, dk, dvalid,
+                       reinterpret_cast<const uint4*>(gt), reinterpret_cast<const uint4*>(qt), dst, dsink);
+    CHECK(hipDeviceSynchronize());
+  }
+  std::vector<uint64_t> st(4 * n);
+  CHECK(hipMemcpy(st.data(), dst, 8 * 4 * n, hipMemcpyDeviceToHost));
+  const char* names[4] = {"inputs", "scalars", "quad_comb", "check"};
+  double sum[4] = {0, 0, 0, 0};
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 4; ++k) sum[k] += st[4 * i + k];
+  printf("{\"geometry\": [%d, %d]", WG, WQ);
+  for (int k = 0; k < 4; ++k) printf(", \"%s_us\": %.2f", names[k], sum[k] / n * 1e3 / rate_khz);
+  printf("}\n");
+  return 0;
+}
