@@ -172,10 +172,12 @@ int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const 
 int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid);
 
 /* Comb-table geometry chosen at registration: window bits of the G table
- * (24 when 4 x its 5.9 GB fit, else 16/20) and of the key tables (the widest
- * of 24 / 22 / 20 / 16 / 12 / 8 whose tables fit the budget: free HBM minus a
- * 64 GiB reserve and the G table, or PBFTV_TABLE_BUDGET_MB), and the HBM bytes
- * the tables occupy per device.  PBFTV_GBITS / PBFTV_QBITS force a pair. */
+ * (16 / 20 / 24 / 26) and of the key tables (24 / 22 / 20 / 16 / 12 / 8) --
+ * the pair with the fewest windows (table additions per verify) whose tables
+ * fit the device's free HBM minus a 64 GiB reserve (an MI355X with 100 keys:
+ * G 26-bit 21.5 GB + keys 22-bit 161 GB); PBFTV_TABLE_BUDGET_MB caps the key
+ * tables, PBFTV_GBITS / PBFTV_QBITS force a width -- and the HBM bytes the
+ * tables occupy per device. */
 int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uint64_t* out_table_bytes);
 
 /* Verify n signatures: hashes (n*32), sig_rs (n*64: r||s big-endian),
