@@ -81,12 +81,14 @@ int pbftv_stream_sync(pbftv_ctx* ctx, int dev);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every
  * kernel launch while enabled.  kernel: 0 = ecdsa scalars, 1 = ecdsa comb,
- * 2 = sha256, 3 = ecdsa wave-per-signature (small batches).  pbftv_kernel_time_ms synchronises the device's stream and
+ * 2 = sha256, 3 = ecdsa wave-per-signature (small batches), 4 = Go-JSON message
+ * encoder (digest / flush batches).  pbftv_kernel_time_ms synchronises the device's stream and
  * returns the summed milliseconds and the launch count since the last reset. */
 #define PBFTV_K_ECDSA_SCALARS 0
 #define PBFTV_K_ECDSA_COMB 1
 #define PBFTV_K_SHA256 2
 #define PBFTV_K_ECDSA_WAVE 3
+#define PBFTV_K_GOJSON 4
 int pbftv_set_kernel_timing(pbftv_ctx* ctx, int enable);
 int pbftv_kernel_time_ms(pbftv_ctx* ctx, int dev, int kernel, double* out_ms, uint64_t* out_launches);
 int pbftv_reset_kernel_times(pbftv_ctx* ctx);
@@ -132,17 +134,21 @@ uint64_t pbftv_gojson_preprepare(int64_t view_id, int64_t sequence_id, const cha
                                  uint64_t req_client_id_len, const char* req_operation, uint64_t req_operation_len,
                                  int64_t req_sequence_id, uint8_t* out, uint64_t cap);
 
-/* digest(*RequestMsg) for n requests: Go-JSON preimages built on the host,
- * hashed in one GPU batch.  client_ids/operations are concatenated byte
- * strings with per-item offsets/lengths.  out_digests: n*32 raw bytes. */
+/* digest(*RequestMsg) for n requests (pbft_impl.go:235-243, called from
+ * StartConsensus :73 and verifyMsg :190): the struct fields are shipped
+ * column-wise, the Go-JSON preimages are built on the GPU (one lane per
+ * message, same encoder as pbftv_gojson_*) and hashed there.  client_ids /
+ * operations are concatenated byte strings with per-item offsets/lengths.
+ * out_digests: n*32 raw bytes. */
 int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
                                const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
                                const uint64_t* operation_off, const uint32_t* operation_len,
                                const int64_t* sequence_ids, uint8_t* out_digests);
 
-/* digest(*VoteMsg) / digest(*ReplyMsg) for n messages (the signed preimages of
- * prepare/commit votes and replies): Go-JSON built on the host, one GPU SHA-256
- * batch.  Byte strings are concatenated with per-item offsets/lengths. */
+/* digest(*VoteMsg) / digest(*ReplyMsg) / digest(*PrePrepareMsg) for n
+ * messages (the signed preimages of votes, replies and pre-prepares): Go-JSON
+ * built on the GPU, hashed there.  For pre-prepares, has_request[i] = 0 encodes
+ * requestMsg as null (the req_* columns must still hold n entries). */
 int pbftv_digest_vote_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
                             const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
                             const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
@@ -152,6 +158,35 @@ int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids
                              const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
                              const uint8_t* results, const uint64_t* result_off, const uint32_t* result_len,
                              uint8_t* out_digests);
+int pbftv_digest_preprepare_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                                  const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                                  const uint8_t* has_request, const int64_t* req_timestamps,
+                                  const uint8_t* req_client_ids, const uint64_t* req_client_id_off,
+                                  const uint32_t* req_client_id_len, const uint8_t* req_operations,
+                                  const uint64_t* req_operation_off, const uint32_t* req_operation_len,
+                                  const int64_t* req_sequence_ids, uint8_t* out_digests);
+
+/* Pool flush of a snapshot of prepare/commit votes (GetAllPrepareMsg /
+ * GetAllCommitMsg, pool/preparePool.go:56-67, pool/commitPool.go:57-68, as
+ * drained by resolvePrepareMsg / resolveCommitMsg, pbft/network/node.go:559-598)
+ * across any number of consensus states, in one GPU round trip per device:
+ *   h_i        = SHA-256(Go-JSON(VoteMsg i))                 -> out_digests (n*32, optional)
+ *   sig bit i  = crypto/ecdsa.Verify(key[key_idx[i]], h_i, r_i, s_i)
+ *                                                            -> out_sig_bitmap (optional;
+ *                                                               needs sig_rs n*64 BE, key_idx)
+ *   msg bit i  = State.verifyMsg(view_ids[i], sequence_ids[i], digest_i) against the
+ *                state state_idx[i] < n_states = (state_view_ids, state_last_seqs,
+ *                32-B request digest)                        -> out_msg_bitmap (optional)
+ * (pbft_impl.go:176-202; a state_idx out of range gives 0).  Bitmaps are
+ * ceil(n/8) bytes, LSB-first.  A vote counts toward its state's quorum iff both
+ * bits are set. */
+int pbftv_flush_votes(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                      const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                      const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                      const int64_t* msg_types, const uint8_t* sig_rs, const uint32_t* key_idx, uint32_t n_states,
+                      const int64_t* state_view_ids, const int64_t* state_last_seqs,
+                      const uint8_t* state_req_digests, const uint32_t* state_idx, uint8_t* out_digests,
+                      uint8_t* out_sig_bitmap, uint8_t* out_msg_bitmap);
 
 /* State.verifyMsg (pbft_impl.go:176-202) over n votes against one state:
  * bit i = view_ids[i] == state_view_id

@@ -1,0 +1,192 @@
+// gojson_enc.h -- Go 1.19 encoding/json.Marshal of the reference's message
+// structs, written once for the host (gojson.cpp) and the gfx950 encoder
+// kernels (gojson_kernels.hip).
+//
+// Restates, byte for byte:
+//   pbft/consensus/pbft_msg_types.go:3-38  field order and tags; the embedded
+//                                          MsgType encodes as "msgType":<int>
+//   encoding/json (go1.19) encodeState.string(escapeHTML=true):
+//     '"' '\\' -> \" \\ ; '\n' '\r' '\t' -> \n \r \t ; other bytes < 0x20 and
+//     '<' '>' '&' -> \u00XX (lowercase hex); each byte of an invalid UTF-8
+//     sequence -> \ufffd (utf8.DecodeRuneInString rules: no overlongs, no
+//     surrogates, nothing above U+10FFFF); U+2028 / U+2029 -> \u2028 / \u2029;
+//     every other byte is copied
+//   strconv.AppendInt(.., 10) for int64 fields; compact output, no newline.
+//
+// A Sink is anything with  void put(uint8_t)  and  uint8_t* grow(uint32_t k)
+// (append k bytes, return where they start).  Output bound (used by the
+// device encoder to place each message in its own slot): a string of n bytes
+// encodes to at most 6n + 2 bytes, an int64 to at most 20.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PBFTV_GJ __host__ __device__ __forceinline__
+#else
+#define PBFTV_GJ inline
+#endif
+
+namespace pbftv {
+namespace gojson {
+
+PBFTV_GJ char hex_lower(uint32_t v) { return (char)(v < 10 ? '0' + v : 'a' + (v - 10)); }
+
+template <class S>
+PBFTV_GJ void lit(S& o, const char* s) {
+  while (*s) o.put((uint8_t)*s++);
+}
+
+template <class S>
+PBFTV_GJ void put_int(S& o, int64_t v) {
+  uint64_t u = v < 0 ? 0 - (uint64_t)v : (uint64_t)v;
+  uint32_t nd = 1;
+  for (uint64_t p = 10; nd < 20 && u >= p; p *= 10) ++nd;  // 10^19 < 2^64: nd reaches 20 only past it
+  uint8_t* w = o.grow(nd + (v < 0 ? 1u : 0u));
+  if (v < 0) *w++ = '-';
+  for (uint32_t k = nd; k-- > 0;) {
+    w[k] = (uint8_t)('0' + (uint32_t)(u % 10));
+    u /= 10;
+  }
+}
+
+PBFTV_GJ bool utf8_cont(uint8_t b) { return (b & 0xC0) == 0x80; }
+
+// length of the valid UTF-8 sequence starting at s[0] (b0 >= 0x80), 0 if
+// invalid; *rune set for 2- and 3-byte sequences (4-byte ones are never U+2028/9)
+PBFTV_GJ uint32_t utf8_len(const uint8_t* s, uint64_t rem, uint32_t* rune) {
+  const uint8_t b0 = s[0];
+  if (b0 >= 0xC2 && b0 <= 0xDF) {
+    if (rem < 2 || !utf8_cont(s[1])) return 0;
+    *rune = ((uint32_t)(b0 & 0x1F) << 6) | (s[1] & 0x3F);
+    return 2;
+  }
+  if (b0 >= 0xE0 && b0 <= 0xEF) {
+    const uint8_t lo = b0 == 0xE0 ? 0xA0 : 0x80, hi = b0 == 0xED ? 0x9F : 0xBF;
+    if (rem < 3 || s[1] < lo || s[1] > hi || !utf8_cont(s[2])) return 0;
+    *rune = ((uint32_t)(b0 & 0x0F) << 12) | ((uint32_t)(s[1] & 0x3F) << 6) | (s[2] & 0x3F);
+    return 3;
+  }
+  if (b0 >= 0xF0 && b0 <= 0xF4) {
+    const uint8_t lo = b0 == 0xF0 ? 0x90 : 0x80, hi = b0 == 0xF4 ? 0x8F : 0xBF;
+    if (rem < 4 || s[1] < lo || s[1] > hi || !utf8_cont(s[2]) || !utf8_cont(s[3])) return 0;
+    *rune = 0x10000;
+    return 4;
+  }
+  return 0;  // continuation byte, C0/C1, F5..FF
+}
+
+template <class S>
+PBFTV_GJ void put_string(S& o, const uint8_t* s, uint64_t n) {
+  o.put('"');
+  uint64_t i = 0;
+  while (i < n) {
+    const uint8_t b = s[i];
+    if (b < 0x80) {
+      ++i;
+      if (b >= 0x20 && b != '"' && b != '\\' && b != '<' && b != '>' && b != '&') {
+        o.put(b);
+      } else if (b == '"' || b == '\\') {
+        o.put('\\');
+        o.put(b);
+      } else if (b == '\n' || b == '\r' || b == '\t') {
+        o.put('\\');
+        o.put(b == '\n' ? 'n' : (b == '\r' ? 'r' : 't'));
+      } else {
+        uint8_t* w = o.grow(6);
+        w[0] = '\\'; w[1] = 'u'; w[2] = '0'; w[3] = '0';
+        w[4] = (uint8_t)hex_lower(b >> 4);
+        w[5] = (uint8_t)hex_lower(b & 15);
+      }
+      continue;
+    }
+    uint32_t rune = 0;
+    const uint32_t len = utf8_len(s + i, n - i, &rune);
+    if (len == 0) {  // utf8.RuneError, width 1
+      lit(o, "\\ufffd");
+      ++i;
+    } else if (rune == 0x2028 || rune == 0x2029) {
+      lit(o, "\\u202");
+      o.put((uint8_t)hex_lower(rune & 15));
+      i += len;
+    } else {
+      for (uint32_t k = 0; k < len; ++k) o.put(s[i + k]);
+      i += len;
+    }
+  }
+  o.put('"');
+}
+
+// RequestMsg (pbft_msg_types.go:3-8)
+template <class S>
+PBFTV_GJ void request(S& o, int64_t ts, const uint8_t* cid, uint64_t cidn, const uint8_t* op, uint64_t opn,
+                      int64_t seq) {
+  lit(o, "{\"timestamp\":");
+  put_int(o, ts);
+  lit(o, ",\"clientID\":");
+  put_string(o, cid, cidn);
+  lit(o, ",\"operation\":");
+  put_string(o, op, opn);
+  lit(o, ",\"sequenceID\":");
+  put_int(o, seq);
+  o.put('}');
+}
+PBFTV_GJ uint64_t request_bound(uint64_t cidn, uint64_t opn) { return 97 + 6 * (cidn + opn); }
+
+// VoteMsg (pbft_msg_types.go:25-31)
+template <class S>
+PBFTV_GJ void vote(S& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t dgn, const uint8_t* nid,
+                   uint64_t nidn, int64_t mt) {
+  lit(o, "{\"viewID\":");
+  put_int(o, view);
+  lit(o, ",\"sequenceID\":");
+  put_int(o, seq);
+  lit(o, ",\"digest\":");
+  put_string(o, dg, dgn);
+  lit(o, ",\"nodeID\":");
+  put_string(o, nid, nidn);
+  lit(o, ",\"msgType\":");
+  put_int(o, mt);
+  o.put('}');
+}
+PBFTV_GJ uint64_t vote_bound(uint64_t dgn, uint64_t nidn) { return 120 + 6 * (dgn + nidn); }
+
+// ReplyMsg (pbft_msg_types.go:10-16)
+template <class S>
+PBFTV_GJ void reply(S& o, int64_t view, int64_t ts, const uint8_t* cid, uint64_t cidn, const uint8_t* nid,
+                    uint64_t nidn, const uint8_t* res, uint64_t resn) {
+  lit(o, "{\"viewID\":");
+  put_int(o, view);
+  lit(o, ",\"timestamp\":");
+  put_int(o, ts);
+  lit(o, ",\"clientID\":");
+  put_string(o, cid, cidn);
+  lit(o, ",\"nodeID\":");
+  put_string(o, nid, nidn);
+  lit(o, ",\"result\":");
+  put_string(o, res, resn);
+  o.put('}');
+}
+PBFTV_GJ uint64_t reply_bound(uint64_t cidn, uint64_t nidn, uint64_t resn) { return 102 + 6 * (cidn + nidn + resn); }
+
+// PrePrepareMsg (pbft_msg_types.go:18-23); a nil *RequestMsg encodes as null
+template <class S>
+PBFTV_GJ void preprepare(S& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t dgn, bool has_req,
+                         int64_t rts, const uint8_t* rcid, uint64_t rcidn, const uint8_t* rop, uint64_t ropn,
+                         int64_t rseq) {
+  lit(o, "{\"viewID\":");
+  put_int(o, view);
+  lit(o, ",\"sequenceID\":");
+  put_int(o, seq);
+  lit(o, ",\"digest\":");
+  put_string(o, dg, dgn);
+  lit(o, ",\"requestMsg\":");
+  if (has_req) request(o, rts, rcid, rcidn, rop, ropn, rseq);
+  else lit(o, "null");
+  o.put('}');
+}
+PBFTV_GJ uint64_t preprepare_bound(uint64_t dgn, uint64_t rcidn, uint64_t ropn) {
+  return 92 + 6 * dgn + request_bound(rcidn, ropn);
+}
+
+}  // namespace gojson
+}  // namespace pbftv

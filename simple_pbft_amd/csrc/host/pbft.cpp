@@ -1,6 +1,8 @@
 // pbft.cpp -- see pbft.h.  Reference line numbers refer to /root/reference.
 #include "pbft.h"
 
+#include <algorithm>
+#include <climits>
 #include <stdexcept>
 
 #include "../../../include/pbftv.h"
@@ -80,6 +82,54 @@ std::vector<bool> GpuCrypto::Verify(const std::vector<Digest32>& hashes, const s
   std::vector<bool> out(n);
   for (uint64_t i = 0; i < n; ++i) out[i] = (bm[i / 8] >> (i % 8)) & 1;
   return out;
+}
+
+// one pbftv_flush_votes call: the votes' fields column-wise, Go-JSON + SHA-256 +
+// verifyMsg + ECDSA on the device
+void GpuCrypto::FlushVotes(const std::vector<VoteMsg>& votes, const std::vector<uint32_t>& key_idx,
+                           const std::vector<StateRef>& states, const std::vector<uint32_t>& state_idx,
+                           std::vector<bool>& sig_ok, std::vector<bool>& msg_ok) {
+  const uint64_t n = votes.size();
+  sig_ok.assign(n, false);
+  msg_ok.assign(n, false);
+  if (n == 0) return;
+  std::vector<int64_t> view(n), seq(n), type(n);
+  std::vector<uint8_t> dblob, nblob;
+  std::vector<uint64_t> doff(n), noff(n);
+  std::vector<uint32_t> dlen(n), nlen(n);
+  std::vector<Sig> sigs(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    const VoteMsg& v = votes[i];
+    view[i] = v.ViewID;
+    seq[i] = v.SequenceID;
+    type[i] = v.Type;
+    doff[i] = dblob.size();
+    dlen[i] = (uint32_t)v.Digest.size();
+    dblob.insert(dblob.end(), v.Digest.begin(), v.Digest.end());
+    noff[i] = nblob.size();
+    nlen[i] = (uint32_t)v.NodeID.size();
+    nblob.insert(nblob.end(), v.NodeID.begin(), v.NodeID.end());
+    sigs[i] = v.Signature;
+  }
+  dblob.push_back(0);
+  nblob.push_back(0);
+  const uint32_t k = (uint32_t)states.size();
+  std::vector<int64_t> sv(k + 1), sl(k + 1);
+  std::vector<uint8_t> sd(32 * (k + 1));
+  for (uint32_t s = 0; s < k; ++s) {
+    sv[s] = states[s].view;
+    sl[s] = states[s].last_seq;
+    std::copy(states[s].req_digest.begin(), states[s].req_digest.end(), sd.begin() + 32 * s);
+  }
+  std::vector<uint8_t> sbm((n + 7) / 8 + 1), mbm((n + 7) / 8 + 1);
+  if (pbftv_flush_votes(ctx_, n, view.data(), seq.data(), dblob.data(), doff.data(), dlen.data(), nblob.data(),
+                        noff.data(), nlen.data(), type.data(), sigs[0].data(), key_idx.data(), k, sv.data(), sl.data(),
+                        sd.data(), state_idx.data(), nullptr, sbm.data(), mbm.data()) != PBFTV_OK)
+    throw std::runtime_error(std::string("pbftv_flush_votes: ") + pbftv_last_error());
+  for (uint64_t i = 0; i < n; ++i) {
+    sig_ok[i] = (sbm[i / 8] >> (i % 8)) & 1;
+    msg_ok[i] = (mbm[i / 8] >> (i % 8)) & 1;
+  }
 }
 
 void GpuCrypto::RegisterKeys(const std::vector<std::array<uint8_t, 64>>& pub_xy) {
@@ -306,6 +356,126 @@ Result<std::pair<ReplyMsg, RequestMsg>> State::CommitBatch(Crypto& c, const KeyT
     }
   }
   return {std::nullopt, ""};
+}
+
+// ---------------------------------------------------------------- multi-state flush
+void Crypto::FlushVotes(const std::vector<VoteMsg>& votes, const std::vector<uint32_t>& key_idx,
+                        const std::vector<StateRef>& states, const std::vector<uint32_t>& state_idx,
+                        std::vector<bool>& sig_ok, std::vector<bool>& msg_ok) {
+  const size_t n = votes.size();
+  std::vector<std::vector<uint8_t>> pre(n);
+  std::vector<Sig> sigs(n);
+  for (size_t i = 0; i < n; ++i) {
+    pre[i] = Marshal(votes[i]);
+    sigs[i] = votes[i].Signature;
+  }
+  sig_ok = n ? Verify(Sha256(pre), sigs, key_idx) : std::vector<bool>();
+  msg_ok.assign(n, false);
+  for (size_t i = 0; i < n; ++i) {
+    if (state_idx[i] >= states.size()) continue;
+    const StateRef& s = states[state_idx[i]];
+    msg_ok[i] = votes[i].ViewID == s.view && (s.last_seq == -1 || s.last_seq < votes[i].SequenceID) &&
+                votes[i].Digest == ToHex(s.req_digest);
+  }
+}
+
+static Digest32 from_hex(const std::string& h) {
+  Digest32 d{};
+  auto nib = [](char c) { return (uint8_t)(c <= '9' ? c - '0' : c - 'a' + 10); };
+  for (int i = 0; i < 32 && 2 * i + 1 < (int)h.size(); ++i) d[i] = (uint8_t)(nib(h[2 * i]) << 4 | nib(h[2 * i + 1]));
+  return d;
+}
+
+State& ConsensusTable::Open(int64_t sequenceID) {
+  auto it = states_.find(sequenceID);
+  if (it == states_.end()) it = states_.emplace(sequenceID, State::CreateState(view_, last_committed_)).first;
+  return it->second;
+}
+
+State* ConsensusTable::Find(int64_t sequenceID) {
+  auto it = states_.find(sequenceID);
+  return it == states_.end() ? nullptr : &it->second;
+}
+
+ConsensusTable::FlushOutcome ConsensusTable::FlushPrepares(Crypto& c, const KeyTable& keys,
+                                                           const std::vector<VoteMsg>& snapshot) {
+  return flush(c, keys, snapshot, false);
+}
+
+ConsensusTable::FlushOutcome ConsensusTable::FlushCommits(Crypto& c, const KeyTable& keys,
+                                                          const std::vector<VoteMsg>& snapshot) {
+  return flush(c, keys, snapshot, true);
+}
+
+ConsensusTable::FlushOutcome ConsensusTable::flush(Crypto& c, const KeyTable& keys, const std::vector<VoteMsg>& snap,
+                                                   bool commit) {
+  const size_t n = snap.size();
+  FlushOutcome o;
+  o.accepted.assign(n, false);
+  o.applied.assign(n, false);
+  o.errors.assign(n, "");
+  // route every vote to its sequence's state; each state's request is hashed once
+  std::map<int64_t, uint32_t> ref_of;
+  std::vector<Crypto::StateRef> refs;
+  std::vector<uint32_t> st_idx(n, UINT32_MAX), kidx(n, 0);
+  std::vector<bool> known(n, false);
+  for (size_t i = 0; i < n; ++i) {
+    auto it = states_.find(snap[i].SequenceID);
+    if (it != states_.end()) {
+      auto ins = ref_of.emplace(it->first, (uint32_t)refs.size());
+      if (ins.second) {
+        State& s = it->second;
+        refs.push_back({s.ViewID, s.LastSequenceID, from_hex(s.request_digest(c))});
+      }
+      st_idx[i] = ins.first->second;
+    }
+    if (auto k = keys.Find(snap[i].NodeID)) {
+      kidx[i] = *k;
+      known[i] = true;
+    }
+  }
+  std::vector<bool> sig_ok, msg_ok;
+  if (n) c.FlushVotes(snap, kidx, refs, st_idx, sig_ok, msg_ok);
+  const std::string what = commit ? "commit" : "prepare";
+  for (size_t i = 0; i < n; ++i) {
+    const bool m = st_idx[i] != UINT32_MAX && msg_ok[i];
+    const bool sg = known[i] && sig_ok[i];
+    o.accepted[i] = m && sg;
+    if (!m) o.errors[i] = what + " message is corrupted";  // pbft_impl.go:117,147
+    else if (!sg) o.errors[i] = what + " message signature is invalid";
+    if (!o.accepted[i]) continue;
+    State& s = states_.at(snap[i].SequenceID);
+    // only a state at this vote's stage takes it; once it advances it stops
+    // taking this snapshot's votes (MSGENOUGH, node.go:564-566, 585-587)
+    if (s.CurrentStage != (commit ? Stage::Prepared : Stage::PrePrepared)) continue;
+    o.applied[i] = true;
+    if (!commit) {
+      s.MsgLogs_.PrepareMsgs[snap[i].NodeID] = snap[i];
+      if (s.prepared()) {
+        s.CurrentStage = Stage::Prepared;
+        VoteMsg v;
+        v.ViewID = s.ViewID;
+        v.SequenceID = snap[i].SequenceID;
+        v.Digest = snap[i].Digest;
+        v.Type = CommitMsg;
+        o.commits.push_back(v);
+      }
+    } else {
+      s.MsgLogs_.CommitMsgs[snap[i].NodeID] = snap[i];
+      if (s.committed()) {
+        s.CurrentStage = Stage::Committed;
+        s.LastSequenceID = snap[i].SequenceID;
+        last_committed_ = std::max(last_committed_, snap[i].SequenceID);
+        ReplyMsg r;
+        r.ViewID = s.ViewID;
+        r.Timestamp = s.MsgLogs_.ReqMsg->Timestamp;
+        r.ClientID = s.MsgLogs_.ReqMsg->ClientID;
+        r.Result = "Executed";
+        o.replies.emplace_back(r, *s.MsgLogs_.ReqMsg);
+      }
+    }
+  }
+  return o;
 }
 
 }  // namespace pbft

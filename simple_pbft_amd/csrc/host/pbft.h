@@ -95,6 +95,18 @@ class Crypto {
   virtual std::vector<bool> Verify(const std::vector<Digest32>& hashes, const std::vector<Sig>& sigs,
                                    const std::vector<uint32_t>& key_idx) = 0;
   virtual void RegisterKeys(const std::vector<std::array<uint8_t, 64>>& pub_xy) = 0;
+  // One pool flush over votes addressed to several consensus states (state i =
+  // view, last sequence, 32-B request digest): sig_ok[j] = valid signature by
+  // key_idx[j] over SHA-256(Marshal(votes[j])); msg_ok[j] = verifyMsg against
+  // states[state_idx[j]].  The default composes Sha256 + Verify + a host
+  // verifyMsg; GpuCrypto does it in one device round trip (pbftv_flush_votes).
+  struct StateRef {
+    int64_t view, last_seq;
+    Digest32 req_digest;
+  };
+  virtual void FlushVotes(const std::vector<VoteMsg>& votes, const std::vector<uint32_t>& key_idx,
+                          const std::vector<StateRef>& states, const std::vector<uint32_t>& state_idx,
+                          std::vector<bool>& sig_ok, std::vector<bool>& msg_ok);
 };
 
 class GpuCrypto : public Crypto {
@@ -105,6 +117,9 @@ class GpuCrypto : public Crypto {
   std::vector<bool> Verify(const std::vector<Digest32>& hashes, const std::vector<Sig>& sigs,
                            const std::vector<uint32_t>& key_idx) override;
   void RegisterKeys(const std::vector<std::array<uint8_t, 64>>& pub_xy) override;
+  void FlushVotes(const std::vector<VoteMsg>& votes, const std::vector<uint32_t>& key_idx,
+                  const std::vector<StateRef>& states, const std::vector<uint32_t>& state_idx,
+                  std::vector<bool>& sig_ok, std::vector<bool>& msg_ok) override;
   pbftv_ctx* ctx() const { return ctx_; }
 
  private:
@@ -188,10 +203,48 @@ class State {
   bool committed() const;  // :222-232
 
  private:
+  friend class ConsensusTable;
   std::optional<std::string> req_digest_;  // digest(ReqMsg), computed once per request
   const std::string& request_digest(Crypto& c);
   std::vector<bool> verify_votes(Crypto& c, const KeyTable& keys, const std::vector<VoteMsg>& snap,
                                  std::vector<std::string>& errs, const char* what);
+};
+
+// ---- sequence-keyed concurrent consensus -------------
+// The reference runs ONE State per node (node.go:277-296) and keys its vote
+// pools by NodeID, so a flush sees at most n-1 votes.  The author's plan
+// (需要改进的地方.md:14-24) keeps a State per sequence in flight and pools keyed
+// by (sequenceID, NodeID); then one flush covers 2f*k votes of k sequences:
+// ONE Crypto::FlushVotes batch (GPU: Go-JSON + SHA-256 + verifyMsg + ECDSA),
+// after which each vote is applied to its own sequence's State in snapshot
+// order with the reference's rules (store by NodeID, quorum 2f, the state
+// stops taking votes once it advances -- MSGENOUGH, node.go:564-566).
+class ConsensusTable {
+ public:
+  explicit ConsensusTable(int64_t viewID) : view_(viewID) {}
+  // the state of a sequence (created on first use as CreateState(view, last
+  // committed sequence), like createStateForNewConsensus, node.go:277-296)
+  State& Open(int64_t sequenceID);
+  State* Find(int64_t sequenceID);
+  void Erase(int64_t sequenceID) { states_.erase(sequenceID); }
+  size_t Size() const { return states_.size(); }
+  int64_t LastCommitted() const { return last_committed_; }
+
+  struct FlushOutcome {
+    std::vector<bool> accepted;       // per snapshot vote: signature + verifyMsg passed
+    std::vector<bool> applied;        // stored in its state (accepted, and the state had not advanced)
+    std::vector<std::string> errors;  // the reference's error for each rejected vote
+    std::vector<VoteMsg> commits;     // prepare flush: the commit vote of every sequence that became prepared
+    std::vector<std::pair<ReplyMsg, RequestMsg>> replies;  // commit flush: every sequence that committed
+  };
+  FlushOutcome FlushPrepares(Crypto& c, const KeyTable& keys, const std::vector<VoteMsg>& snapshot);
+  FlushOutcome FlushCommits(Crypto& c, const KeyTable& keys, const std::vector<VoteMsg>& snapshot);
+
+ private:
+  FlushOutcome flush(Crypto& c, const KeyTable& keys, const std::vector<VoteMsg>& snap, bool commit);
+  int64_t view_;
+  int64_t last_committed_ = -1;
+  std::map<int64_t, State> states_;
 };
 
 // ---- pool/*.go --------------------------------------------------------
@@ -255,6 +308,12 @@ struct CommitMsgPool : MsgPool<VoteMsg> {
 };
 struct ReplyMsgPool : MsgPool<ReplyMsg> {
   ReplyMsgPool() : MsgPool([](const ReplyMsg& m) { return m.NodeID; }) {}
+};
+
+// sequence-keyed vote pool (ConsensusTable's input): key = "<sequenceID>/<NodeID>",
+// so votes of many sequences coexist and a re-sent vote overwrites its own entry
+struct SeqVotePool : MsgPool<VoteMsg> {
+  SeqVotePool() : MsgPool([](const VoteMsg& m) { return std::to_string(m.SequenceID) + "/" + m.NodeID; }) {}
 };
 
 }  // namespace pbft

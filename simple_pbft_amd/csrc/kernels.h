@@ -60,4 +60,55 @@ hipError_t launch_sha256(const uint8_t* data, const uint64_t* offsets, const uin
 size_t sha256_order_scratch_bytes(uint64_t n);
 hipError_t launch_sha256_order(const uint32_t* lengths, uint64_t n, uint32_t* order, void* scratch, hipStream_t st);
 
+// ---- Go-JSON preimages on the device (gojson_kernels.hip) ----
+// Column-wise message fields (device pointers, n entries each); a string
+// column is a byte blob with per-message offset and length.
+struct StrCol {
+  const uint8_t* data;
+  const uint64_t* off;
+  const uint32_t* len;
+};
+struct RequestCols {
+  const int64_t* ts;
+  StrCol cid, op;
+  const int64_t* seq;
+};
+struct VoteCols {
+  const int64_t* view;
+  const int64_t* seq;
+  StrCol digest, node;
+  const int64_t* type;
+};
+struct ReplyCols {
+  const int64_t* view;
+  const int64_t* ts;
+  StrCol cid, node, result;
+};
+struct PrePrepareCols {
+  const int64_t* view;
+  const int64_t* seq;
+  StrCol digest;
+  const uint8_t* has_req;  // 0: requestMsg is nil (request columns still hold n entries)
+  RequestCols req;
+};
+// consensus states a vote batch is checked against (State.verifyMsg)
+struct StateCols {
+  const int64_t* view;
+  const int64_t* last_seq;
+  const uint8_t* req_digest;  // 32 B per state
+  const uint32_t* idx;        // per vote: its state
+  uint32_t n;
+};
+// Message i's preimage is written at out + slot[i] (slot sized by the
+// gojson_enc.h bound), its length to out_len[i].  launch_gojson_vote also
+// writes msg_ok[i] = verifyMsg result when msg_ok != nullptr.
+hipError_t launch_gojson_request(const RequestCols& c, uint64_t n, const uint64_t* slot, uint8_t* out,
+                                 uint32_t* out_len, hipStream_t st);
+hipError_t launch_gojson_vote(const VoteCols& c, uint64_t n, const uint64_t* slot, uint8_t* out, uint32_t* out_len,
+                              const StateCols& s, uint8_t* msg_ok, hipStream_t st);
+hipError_t launch_gojson_reply(const ReplyCols& c, uint64_t n, const uint64_t* slot, uint8_t* out, uint32_t* out_len,
+                               hipStream_t st);
+hipError_t launch_gojson_preprepare(const PrePrepareCols& c, uint64_t n, const uint64_t* slot, uint8_t* out,
+                                    uint32_t* out_len, hipStream_t st);
+
 }  // namespace pbftv

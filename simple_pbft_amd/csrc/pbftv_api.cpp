@@ -23,6 +23,7 @@
 
 #include "../../include/pbftv.h"
 #include "gojson.h"
+#include "gojson_enc.h"
 #include "kernels.h"
 
 namespace {
@@ -107,12 +108,16 @@ struct Device {
   HostBuf stage;  // zero-copy inputs/outputs of the small-batch path
   // sha scratch
   DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
+  // message batches (Go-JSON on the device): packed column inputs, verifyMsg bytes,
+  // pinned staging for the one H2D and the results
+  DevBuf arena, msgok;
+  HostBuf mstage, mout;
   // kernel timing (events recorded around launches while ctx timing is on)
   const bool* timing = nullptr;
-  static constexpr int kKernels = 4;  // PBFTV_K_*
+  static constexpr int kKernels = 5;  // PBFTV_K_*
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[kKernels];
-  double acc_ms[kKernels] = {0, 0, 0, 0};
-  uint64_t launches[kKernels] = {0, 0, 0, 0};
+  double acc_ms[kKernels] = {0, 0, 0, 0, 0};
+  uint64_t launches[kKernels] = {0, 0, 0, 0, 0};
 };
 
 // record start/stop events around one launch when timing is enabled
@@ -197,6 +202,106 @@ int run_sharded(pbftv_ctx* ctx, uint64_t n, Fn fn) {
 
 hipStream_t pick_stream(Device& d, void* stream) { return stream ? reinterpret_cast<hipStream_t>(stream) : d.stream; }
 
+// ---- message batches: column inputs packed for ONE host->device copy ----
+// Host segments are copied (16-B aligned) into the device's pinned staging
+// buffer, then to its device arena with a single hipMemcpyAsync.
+struct Packer {
+  struct Seg {
+    const void* src;
+    size_t bytes, off;
+  };
+  std::vector<Seg> segs;
+  std::vector<std::vector<uint64_t>> owned;  // rebased offsets, slots (inner buffers stay put when moved)
+  size_t total = 0;
+  size_t add(const void* src, size_t bytes) {
+    const size_t o = total;
+    segs.push_back({src, bytes, o});
+    total = (o + bytes + 15) & ~(size_t)15;
+    return o;
+  }
+  size_t add_owned(std::vector<uint64_t>&& v) {
+    owned.push_back(std::move(v));
+    return add(owned.back().data(), owned.back().size() * 8);
+  }
+  // string column restricted to items [lo, hi): the blob span they use, offsets rebased onto it
+  struct Str {
+    size_t data, off, len;
+  };
+  Str add_str(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint64_t lo, uint64_t hi) {
+    uint64_t a = UINT64_MAX, b = 0;
+    for (uint64_t i = lo; i < hi; ++i)
+      if (len[i]) {
+        a = std::min(a, off[i]);
+        b = std::max(b, off[i] + len[i]);
+      }
+    if (a > b) a = b = 0;
+    std::vector<uint64_t> r(hi - lo);
+    for (uint64_t i = lo; i < hi; ++i) r[i - lo] = len[i] ? off[i] - a : 0;
+    Str s;
+    s.data = add(b > a ? data + a : nullptr, b - a);
+    s.off = add_owned(std::move(r));
+    s.len = add(len + lo, 4 * (hi - lo));
+    return s;
+  }
+};
+
+// pinned copy + one H2D into d.arena (stream-ordered before the kernels that read it)
+int upload(Device& d, const Packer& p) {
+  HIP_TRY(d.mstage.ensure(p.total + 16));
+  HIP_TRY(d.arena.ensure(p.total + 16));
+  uint8_t* h = d.mstage.as<uint8_t>();
+  for (const auto& s : p.segs)
+    if (s.bytes) std::memcpy(h + s.off, s.src, s.bytes);
+  if (p.total) HIP_TRY(hipMemcpyAsync(d.arena.p, h, p.total, hipMemcpyHostToDevice, d.stream));
+  return PBFTV_OK;
+}
+
+template <class T>
+const T* at(const Device& d, size_t off) {
+  return reinterpret_cast<const T*>(d.arena.as<uint8_t>() + off);
+}
+
+pbftv::StrCol str_col(const Device& d, const Packer::Str& s) {
+  return {at<uint8_t>(d, s.data), at<uint64_t>(d, s.off), at<uint32_t>(d, s.len)};
+}
+
+// slot offsets of the preimage buffer from per-item encoder bounds (4-B aligned)
+template <class Bound>
+std::vector<uint64_t> slots(uint64_t lo, uint64_t hi, Bound bound, uint64_t* total) {
+  std::vector<uint64_t> s(hi - lo);
+  uint64_t t = 0;
+  for (uint64_t i = lo; i < hi; ++i) {
+    s[i - lo] = t;
+    t += (bound(i) + 3) & ~3ull;
+  }
+  *total = t;
+  return s;
+}
+
+// encode (launch(slot_dev) writes preimages into d.data, lengths into
+// d.lengths), then SHA-256 of every slot into d.digests
+template <class Launch>
+int encode_and_hash(Device& d, uint64_t m, const uint64_t* slot_dev, uint64_t pre_bytes, Launch launch) {
+  HIP_TRY(d.data.ensure(pre_bytes + 64));
+  HIP_TRY(d.lengths.ensure(m * 4 + 4));
+  HIP_TRY(d.digests.ensure(m * 32 + 32));
+  HIP_TRY(timed(d, PBFTV_K_GOJSON, d.stream, launch));
+  HIP_TRY(timed(d, PBFTV_K_SHA256, d.stream, [&] {
+    return pbftv::launch_sha256(d.data.as<uint8_t>(), slot_dev, d.lengths.as<uint32_t>(), nullptr, m,
+                                d.digests.as<uint8_t>(), nullptr, nullptr, d.stream);
+  }));
+  return PBFTV_OK;
+}
+
+// digests of shard [lo, hi) back to the caller
+int digests_out(Device& d, uint64_t lo, uint64_t m, uint8_t* out) {
+  HIP_TRY(d.mout.ensure(m * 32 + 32));
+  HIP_TRY(hipMemcpyAsync(d.mout.p, d.digests.p, m * 32, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  std::memcpy(out + 32 * lo, d.mout.p, m * 32);
+  return PBFTV_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -248,9 +353,9 @@ void pbftv_close(pbftv_ctx* ctx) {
     for (DevBuf* b : {&d->gtab, &d->qtabs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag, &d->prefix,
                       &d->bitmap,
                       &d->data, &d->offsets, &d->lengths, &d->order, &d->order_scratch, &d->digests, &d->expected,
-                      &d->shabits})
+                      &d->shabits, &d->arena, &d->msgok})
       b->release();
-    d->stage.release();
+    for (HostBuf* b : {&d->stage, &d->mstage, &d->mout}) b->release();
     (void)hipStreamDestroy(d->stream);
   }
   delete ctx;
@@ -742,6 +847,7 @@ int pbftv_hash_hex(pbftv_ctx* ctx, const uint8_t* content, uint64_t len, char ou
   return PBFTV_OK;
 }
 
+// ---- digests of message batches: Go-JSON built on the device, then SHA-256 ----
 int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
                                const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
                                const uint64_t* operation_off, const uint32_t* operation_len,
@@ -750,49 +856,36 @@ int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timest
   if (n && (!timestamps || !client_id_off || !client_id_len || !operation_off || !operation_len || !sequence_ids ||
             !out_digests))
     return fail(PBFTV_EINVAL, "null buffer");
-  std::vector<uint8_t> buf;
-  std::vector<uint64_t> off(n);
-  std::vector<uint32_t> len(n);
-  buf.reserve(n * 112);
-  for (uint64_t i = 0; i < n; ++i) {
-    off[i] = buf.size();
-    pbftv::gojson::append_request(buf, timestamps[i], client_ids + client_id_off[i], client_id_len[i],
-                                  operations + operation_off[i], operation_len[i], sequence_ids[i]);
-    const uint64_t l = buf.size() - off[i];
-    if (l > 0xFFFFFFFFull) return fail(PBFTV_EINVAL, "preimage longer than 4 GiB");
-    len[i] = (uint32_t)l;
-  }
-  return pbftv_sha256_batch(ctx, buf.data(), off.data(), len.data(), n, out_digests);
-}
-
-static int hash_preimages(pbftv_ctx* ctx, const std::vector<uint8_t>& buf, const std::vector<uint64_t>& off,
-                          uint64_t n, uint8_t* out_digests) {
-  std::vector<uint32_t> len(n);
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint64_t l = (i + 1 < n ? off[i + 1] : buf.size()) - off[i];
-    if (l > 0xFFFFFFFFull) return fail(PBFTV_EINVAL, "preimage longer than 4 GiB");
-    len[i] = (uint32_t)l;
-  }
-  return pbftv_sha256_batch(ctx, buf.data(), off.data(), len.data(), n, out_digests);
+  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
+    const uint64_t m = s.hi - s.lo;
+    Packer p;
+    uint64_t pre = 0;
+    const size_t o_slot = p.add_owned(slots(s.lo, s.hi, [&](uint64_t i) {
+      return pbftv::gojson::request_bound(client_id_len[i], operation_len[i]);
+    }, &pre));
+    const size_t o_ts = p.add(timestamps + s.lo, 8 * m), o_seq = p.add(sequence_ids + s.lo, 8 * m);
+    const auto cid = p.add_str(client_ids, client_id_off, client_id_len, s.lo, s.hi);
+    const auto op = p.add_str(operations, operation_off, operation_len, s.lo, s.hi);
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    int rc = upload(d, p);
+    if (rc != PBFTV_OK) return rc;
+    const pbftv::RequestCols c{at<int64_t>(d, o_ts), str_col(d, cid), str_col(d, op), at<int64_t>(d, o_seq)};
+    const uint64_t* slot = at<uint64_t>(d, o_slot);
+    rc = encode_and_hash(d, m, slot, pre, [&] {
+      return pbftv::launch_gojson_request(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), d.stream);
+    });
+    return rc != PBFTV_OK ? rc : digests_out(d, s.lo, m, out_digests);
+  });
 }
 
 int pbftv_digest_vote_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
                             const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
                             const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
                             const int64_t* msg_types, uint8_t* out_digests) {
-  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
-  if (n && (!view_ids || !sequence_ids || !digest_off || !digest_len || !node_id_off || !node_id_len || !msg_types ||
-            !out_digests))
-    return fail(PBFTV_EINVAL, "null buffer");
-  std::vector<uint8_t> buf;
-  std::vector<uint64_t> off(n);
-  buf.reserve(n * 176);
-  for (uint64_t i = 0; i < n; ++i) {
-    off[i] = buf.size();
-    pbftv::gojson::append_vote(buf, view_ids[i], sequence_ids[i], digests + digest_off[i], digest_len[i],
-                               node_ids + node_id_off[i], node_id_len[i], msg_types[i]);
-  }
-  return hash_preimages(ctx, buf, off, n, out_digests);
+  return pbftv_flush_votes(ctx, n, view_ids, sequence_ids, digests, digest_off, digest_len, node_ids, node_id_off,
+                           node_id_len, msg_types, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+                           out_digests, nullptr, nullptr);
 }
 
 int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* timestamps,
@@ -804,15 +897,160 @@ int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids
   if (n && (!view_ids || !timestamps || !client_id_off || !client_id_len || !node_id_off || !node_id_len ||
             !result_off || !result_len || !out_digests))
     return fail(PBFTV_EINVAL, "null buffer");
-  std::vector<uint8_t> buf;
-  std::vector<uint64_t> off(n);
-  buf.reserve(n * 120);
-  for (uint64_t i = 0; i < n; ++i) {
-    off[i] = buf.size();
-    pbftv::gojson::append_reply(buf, view_ids[i], timestamps[i], client_ids + client_id_off[i], client_id_len[i],
-                                node_ids + node_id_off[i], node_id_len[i], results + result_off[i], result_len[i]);
-  }
-  return hash_preimages(ctx, buf, off, n, out_digests);
+  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
+    const uint64_t m = s.hi - s.lo;
+    Packer p;
+    uint64_t pre = 0;
+    const size_t o_slot = p.add_owned(slots(s.lo, s.hi, [&](uint64_t i) {
+      return pbftv::gojson::reply_bound(client_id_len[i], node_id_len[i], result_len[i]);
+    }, &pre));
+    const size_t o_view = p.add(view_ids + s.lo, 8 * m), o_ts = p.add(timestamps + s.lo, 8 * m);
+    const auto cid = p.add_str(client_ids, client_id_off, client_id_len, s.lo, s.hi);
+    const auto nid = p.add_str(node_ids, node_id_off, node_id_len, s.lo, s.hi);
+    const auto res = p.add_str(results, result_off, result_len, s.lo, s.hi);
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    int rc = upload(d, p);
+    if (rc != PBFTV_OK) return rc;
+    const pbftv::ReplyCols c{at<int64_t>(d, o_view), at<int64_t>(d, o_ts), str_col(d, cid), str_col(d, nid),
+                             str_col(d, res)};
+    const uint64_t* slot = at<uint64_t>(d, o_slot);
+    rc = encode_and_hash(d, m, slot, pre, [&] {
+      return pbftv::launch_gojson_reply(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), d.stream);
+    });
+    return rc != PBFTV_OK ? rc : digests_out(d, s.lo, m, out_digests);
+  });
+}
+
+int pbftv_digest_preprepare_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                                  const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                                  const uint8_t* has_request, const int64_t* req_timestamps,
+                                  const uint8_t* req_client_ids, const uint64_t* req_client_id_off,
+                                  const uint32_t* req_client_id_len, const uint8_t* req_operations,
+                                  const uint64_t* req_operation_off, const uint32_t* req_operation_len,
+                                  const int64_t* req_sequence_ids, uint8_t* out_digests) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!view_ids || !sequence_ids || !digest_off || !digest_len || !has_request || !req_timestamps ||
+            !req_client_id_off || !req_client_id_len || !req_operation_off || !req_operation_len ||
+            !req_sequence_ids || !out_digests))
+    return fail(PBFTV_EINVAL, "null buffer");
+  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
+    const uint64_t m = s.hi - s.lo;
+    Packer p;
+    uint64_t pre = 0;
+    const size_t o_slot = p.add_owned(slots(s.lo, s.hi, [&](uint64_t i) {
+      return pbftv::gojson::preprepare_bound(digest_len[i], has_request[i] ? req_client_id_len[i] : 0,
+                                             has_request[i] ? req_operation_len[i] : 0);
+    }, &pre));
+    const size_t o_view = p.add(view_ids + s.lo, 8 * m), o_seq = p.add(sequence_ids + s.lo, 8 * m);
+    const size_t o_has = p.add(has_request + s.lo, m);
+    const size_t o_rts = p.add(req_timestamps + s.lo, 8 * m), o_rseq = p.add(req_sequence_ids + s.lo, 8 * m);
+    const auto dg = p.add_str(digests, digest_off, digest_len, s.lo, s.hi);
+    const auto cid = p.add_str(req_client_ids, req_client_id_off, req_client_id_len, s.lo, s.hi);
+    const auto op = p.add_str(req_operations, req_operation_off, req_operation_len, s.lo, s.hi);
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    int rc = upload(d, p);
+    if (rc != PBFTV_OK) return rc;
+    const pbftv::PrePrepareCols c{
+        at<int64_t>(d, o_view), at<int64_t>(d, o_seq), str_col(d, dg), at<uint8_t>(d, o_has),
+        {at<int64_t>(d, o_rts), str_col(d, cid), str_col(d, op), at<int64_t>(d, o_rseq)}};
+    const uint64_t* slot = at<uint64_t>(d, o_slot);
+    rc = encode_and_hash(d, m, slot, pre, [&] {
+      return pbftv::launch_gojson_preprepare(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), d.stream);
+    });
+    return rc != PBFTV_OK ? rc : digests_out(d, s.lo, m, out_digests);
+  });
+}
+
+// Pool flush of a vote snapshot: Go-JSON + SHA-256 + verifyMsg + ECDSA in one
+// device round trip per shard (see pbftv.h).  Also the body of
+// pbftv_digest_vote_batch (no signatures, no states).
+int pbftv_flush_votes(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                      const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                      const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                      const int64_t* msg_types, const uint8_t* sig_rs, const uint32_t* key_idx, uint32_t n_states,
+                      const int64_t* state_view_ids, const int64_t* state_last_seqs,
+                      const uint8_t* state_req_digests, const uint32_t* state_idx, uint8_t* out_digests,
+                      uint8_t* out_sig_bitmap, uint8_t* out_msg_bitmap) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!view_ids || !sequence_ids || !digest_off || !digest_len || !node_id_off || !node_id_len || !msg_types))
+    return fail(PBFTV_EINVAL, "null buffer");
+  const bool sig = out_sig_bitmap != nullptr, msg = out_msg_bitmap != nullptr;
+  if (n && sig && (!sig_rs || !key_idx)) return fail(PBFTV_EINVAL, "signatures requested without sig_rs/key_idx");
+  if (n && msg && (!state_idx || (n_states && (!state_view_ids || !state_last_seqs || !state_req_digests))))
+    return fail(PBFTV_EINVAL, "verifyMsg requested without states");
+  if (sig)
+    for (auto& dp : ctx->devs)
+      if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
+    const uint64_t m = s.hi - s.lo;
+    Packer p;
+    uint64_t pre = 0;
+    const size_t o_slot = p.add_owned(slots(s.lo, s.hi, [&](uint64_t i) {
+      return pbftv::gojson::vote_bound(digest_len[i], node_id_len[i]);
+    }, &pre));
+    const size_t o_view = p.add(view_ids + s.lo, 8 * m), o_seq = p.add(sequence_ids + s.lo, 8 * m),
+                 o_type = p.add(msg_types + s.lo, 8 * m);
+    const auto dg = p.add_str(digests, digest_off, digest_len, s.lo, s.hi);
+    const auto nid = p.add_str(node_ids, node_id_off, node_id_len, s.lo, s.hi);
+    size_t o_sig = 0, o_key = 0, o_sv = 0, o_sl = 0, o_sd = 0, o_si = 0;
+    if (sig) {
+      o_sig = p.add(sig_rs + 64 * s.lo, 64 * m);
+      o_key = p.add(key_idx + s.lo, 4 * m);
+    }
+    if (msg) {
+      o_sv = p.add(state_view_ids, 8ull * n_states);
+      o_sl = p.add(state_last_seqs, 8ull * n_states);
+      o_sd = p.add(state_req_digests, 32ull * n_states);
+      o_si = p.add(state_idx + s.lo, 4 * m);
+    }
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    int rc = upload(d, p);
+    if (rc != PBFTV_OK) return rc;
+    const pbftv::VoteCols c{at<int64_t>(d, o_view), at<int64_t>(d, o_seq), str_col(d, dg), str_col(d, nid),
+                            at<int64_t>(d, o_type)};
+    pbftv::StateCols sc{nullptr, nullptr, nullptr, nullptr, n_states};
+    uint8_t* msgok = nullptr;
+    if (msg) {
+      sc = {at<int64_t>(d, o_sv), at<int64_t>(d, o_sl), at<uint8_t>(d, o_sd), at<uint32_t>(d, o_si), n_states};
+      HIP_TRY(d.msgok.ensure(m + 8));
+      msgok = d.msgok.as<uint8_t>();
+    }
+    const uint64_t* slot = at<uint64_t>(d, o_slot);
+    rc = encode_and_hash(d, m, slot, pre, [&] {
+      return pbftv::launch_gojson_vote(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), sc, msgok,
+                                       d.stream);
+    });
+    if (rc != PBFTV_OK) return rc;
+    const uint64_t nb = (m + 7) / 8;
+    if (sig) {
+      HIP_TRY(d.bitmap.ensure(nb + 8));
+      rc = verify_on_device(d, d.digests.as<uint8_t>(), at<uint8_t>(d, o_sig), at<uint32_t>(d, o_key), m,
+                            d.bitmap.as<uint8_t>(), d.stream);
+      if (rc != PBFTV_OK) return rc;
+    }
+    // results: digests | signature bitmap | verifyMsg bytes
+    const size_t r_dg = 0, r_sig = out_digests ? 32 * m : 0, r_msg = r_sig + (sig ? nb : 0);
+    HIP_TRY(d.mout.ensure(r_msg + (msg ? m : 0) + 16));
+    uint8_t* h = d.mout.as<uint8_t>();
+    if (out_digests) HIP_TRY(hipMemcpyAsync(h + r_dg, d.digests.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+    if (sig) HIP_TRY(hipMemcpyAsync(h + r_sig, d.bitmap.p, nb, hipMemcpyDeviceToHost, d.stream));
+    if (msg) HIP_TRY(hipMemcpyAsync(h + r_msg, msgok, m, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    if (out_digests) std::memcpy(out_digests + 32 * s.lo, h + r_dg, 32 * m);
+    if (sig) {
+      std::memcpy(out_sig_bitmap + s.lo / 8, h + r_sig, nb);
+      if (m % 8) out_sig_bitmap[s.lo / 8 + nb - 1] &= (uint8_t)((1u << (m % 8)) - 1u);
+    }
+    if (msg) {
+      uint8_t* bm = out_msg_bitmap + s.lo / 8;
+      std::memset(bm, 0, nb);
+      for (uint64_t i = 0; i < m; ++i) bm[i >> 3] |= (uint8_t)((h[r_msg + i] & 1u) << (i & 7));
+    }
+    return PBFTV_OK;
+  });
 }
 
 int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const uint8_t req_digest[32], uint64_t n,

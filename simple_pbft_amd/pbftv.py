@@ -89,6 +89,8 @@ def lib() -> ctypes.CDLL:
                                                       _vp]),
         "pbftv_digest_vote_batch": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 10),
         "pbftv_digest_reply_batch": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 12),
+        "pbftv_digest_preprepare_batch": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 15),
+        "pbftv_flush_votes": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 11 + [ctypes.c_uint32] + [_vp] * 7),
         "pbftv_verify_msg_batch": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _vp, ctypes.c_uint64, _vp, _vp,
                                                   _vp, _vp, _vp, _vp]),
         "pbftv_register_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
@@ -199,6 +201,63 @@ K_ECDSA_SCALARS = 0
 K_ECDSA_COMB = 1
 K_SHA256 = 2
 K_ECDSA_WAVE = 3
+K_GOJSON = 4
+
+
+class RequestColumns:
+    """RequestMsgs (pbft_msg_types.go:3-8) column-wise for pbftv_digest_request_batch."""
+
+    def __init__(self, requests):
+        """requests: list of (timestamp, clientID bytes, operation bytes, sequenceID)."""
+        self.n = len(requests)
+        self.ts = np.array([r[0] for r in requests], np.int64)
+        self.seq = np.array([r[3] for r in requests], np.int64)
+        self.cid = Verifier.pack([r[1] for r in requests])
+        self.op = Verifier.pack([r[2] for r in requests])
+
+    def args(self):
+        (cb, co, cl), (ob, oo, ol) = self.cid, self.op
+        return [self.ts.ctypes.data, cb.ctypes.data, co.ctypes.data, cl.ctypes.data, ob.ctypes.data, oo.ctypes.data,
+                ol.ctypes.data, self.seq.ctypes.data]
+
+
+class ReplyColumns:
+    """ReplyMsgs (pbft_msg_types.go:10-16) column-wise for pbftv_digest_reply_batch."""
+
+    def __init__(self, replies):
+        """replies: list of (viewID, timestamp, clientID bytes, nodeID bytes, result bytes)."""
+        self.n = len(replies)
+        self.view = np.array([x[0] for x in replies], np.int64)
+        self.ts = np.array([x[1] for x in replies], np.int64)
+        self.cid = Verifier.pack([x[2] for x in replies])
+        self.node = Verifier.pack([x[3] for x in replies])
+        self.result = Verifier.pack([x[4] for x in replies])
+
+    def args(self):
+        out = [self.view.ctypes.data, self.ts.ctypes.data]
+        for b, o, ln in (self.cid, self.node, self.result):
+            out += [b.ctypes.data, o.ctypes.data, ln.ctypes.data]
+        return out
+
+
+class VoteColumns:
+    """A snapshot of VoteMsgs (pbft_msg_types.go:25-31) laid out column-wise, as
+    the cgo shim would hand a pool snapshot to pbftv_flush_votes: int64 columns
+    plus byte-string blobs with per-vote offsets/lengths."""
+
+    def __init__(self, votes):
+        """votes: list of (viewID, sequenceID, digest bytes, nodeID bytes, msgType)."""
+        self.n = len(votes)
+        self.view = np.array([x[0] for x in votes], np.int64)
+        self.seq = np.array([x[1] for x in votes], np.int64)
+        self.type = np.array([x[4] for x in votes], np.int64)
+        self.digest = Verifier.pack([x[2] for x in votes])
+        self.node = Verifier.pack([x[3] for x in votes])
+
+    def args(self):
+        (db, do, dl), (nb, no, nl) = self.digest, self.node
+        return [self.view.ctypes.data, self.seq.ctypes.data, db.ctypes.data, do.ctypes.data, dl.ctypes.data,
+                nb.ctypes.data, no.ctypes.data, nl.ctypes.data, self.type.ctypes.data]
 
 
 class DeviceBuffer:
@@ -333,47 +392,73 @@ class Verifier:
         return bitmap_to_bool(bm, n)
 
     def digest_request_batch(self, requests) -> np.ndarray:
-        """requests: list of (timestamp, clientID bytes, operation bytes, sequenceID)."""
-        n = len(requests)
-        ts = np.array([r[0] for r in requests], np.int64)
-        seq = np.array([r[3] for r in requests], np.int64)
-        cid_blob, cid_off, cid_len = self.pack([r[1] for r in requests])
-        op_blob, op_off, op_len = self.pack([r[2] for r in requests])
-        out = np.zeros((max(n, 1), 32), np.uint8)
-        _check(self._L.pbftv_digest_request_batch(self._h, n, ts.ctypes.data, cid_blob.ctypes.data,
-                                                  cid_off.ctypes.data, cid_len.ctypes.data, op_blob.ctypes.data,
-                                                  op_off.ctypes.data, op_len.ctypes.data, seq.ctypes.data,
-                                                  out.ctypes.data))
-        return out[:n]
+        """requests: RequestColumns, or a list of (timestamp, clientID bytes, operation bytes, sequenceID)."""
+        cols = requests if isinstance(requests, RequestColumns) else RequestColumns(requests)
+        out = np.zeros((max(cols.n, 1), 32), np.uint8)
+        _check(self._L.pbftv_digest_request_batch(self._h, cols.n, *cols.args(), out.ctypes.data))
+        return out[:cols.n]
 
     def digest_vote_batch(self, votes) -> np.ndarray:
-        """votes: list of (viewID, sequenceID, digest bytes, nodeID bytes, msgType)."""
-        n = len(votes)
-        v = np.array([x[0] for x in votes], np.int64)
-        q = np.array([x[1] for x in votes], np.int64)
-        mt = np.array([x[4] for x in votes], np.int64)
-        db, do, dl = self.pack([x[2] for x in votes])
-        nb, no, nl = self.pack([x[3] for x in votes])
-        out = np.zeros((max(n, 1), 32), np.uint8)
-        _check(self._L.pbftv_digest_vote_batch(self._h, n, v.ctypes.data, q.ctypes.data, db.ctypes.data,
-                                               do.ctypes.data, dl.ctypes.data, nb.ctypes.data, no.ctypes.data,
-                                               nl.ctypes.data, mt.ctypes.data, out.ctypes.data))
-        return out[:n]
+        """votes: VoteColumns, or a list of (viewID, sequenceID, digest bytes, nodeID bytes, msgType)."""
+        cols = votes if isinstance(votes, VoteColumns) else VoteColumns(votes)
+        out = np.zeros((max(cols.n, 1), 32), np.uint8)
+        _check(self._L.pbftv_digest_vote_batch(self._h, cols.n, *cols.args(), out.ctypes.data))
+        return out[:cols.n]
 
     def digest_reply_batch(self, replies) -> np.ndarray:
-        """replies: list of (viewID, timestamp, clientID bytes, nodeID bytes, result bytes)."""
-        n = len(replies)
-        v = np.array([x[0] for x in replies], np.int64)
-        t = np.array([x[1] for x in replies], np.int64)
-        cb, co, cl = self.pack([x[2] for x in replies])
-        nb, no, nl = self.pack([x[3] for x in replies])
-        rb, ro, rl = self.pack([x[4] for x in replies])
+        """replies: ReplyColumns, or a list of (viewID, timestamp, clientID bytes, nodeID bytes, result bytes)."""
+        cols = replies if isinstance(replies, ReplyColumns) else ReplyColumns(replies)
+        out = np.zeros((max(cols.n, 1), 32), np.uint8)
+        _check(self._L.pbftv_digest_reply_batch(self._h, cols.n, *cols.args(), out.ctypes.data))
+        return out[:cols.n]
+
+    def digest_preprepare_batch(self, pps) -> np.ndarray:
+        """pps: list of (viewID, sequenceID, digest bytes, request) with request
+        None (requestMsg nil) or (timestamp, clientID bytes, operation bytes, sequenceID)."""
+        n = len(pps)
+        v = np.array([x[0] for x in pps], np.int64)
+        q = np.array([x[1] for x in pps], np.int64)
+        has = np.array([x[3] is not None for x in pps], np.uint8)
+        reqs = [x[3] if x[3] is not None else (0, b"", b"", 0) for x in pps]
+        rts = np.array([r[0] for r in reqs], np.int64)
+        rsq = np.array([r[3] for r in reqs], np.int64)
+        db, do, dl = self.pack([x[2] for x in pps])
+        cb, co, cl = self.pack([r[1] for r in reqs])
+        ob, oo, ol = self.pack([r[2] for r in reqs])
         out = np.zeros((max(n, 1), 32), np.uint8)
-        _check(self._L.pbftv_digest_reply_batch(self._h, n, v.ctypes.data, t.ctypes.data, cb.ctypes.data,
-                                                co.ctypes.data, cl.ctypes.data, nb.ctypes.data, no.ctypes.data,
-                                                nl.ctypes.data, rb.ctypes.data, ro.ctypes.data, rl.ctypes.data,
-                                                out.ctypes.data))
+        _check(self._L.pbftv_digest_preprepare_batch(self._h, n, v.ctypes.data, q.ctypes.data, db.ctypes.data,
+                                                     do.ctypes.data, dl.ctypes.data, has.ctypes.data, rts.ctypes.data,
+                                                     cb.ctypes.data, co.ctypes.data, cl.ctypes.data, ob.ctypes.data,
+                                                     oo.ctypes.data, ol.ctypes.data, rsq.ctypes.data,
+                                                     out.ctypes.data))
         return out[:n]
+
+    def flush_votes(self, cols: "VoteColumns", sigs=None, key_idx=None, states=None, state_idx=None,
+                    digests: bool = True):
+        """pbftv_flush_votes: (digests | None, sig_ok | None, msg_ok | None).
+        states: (view_ids int64[k], last_seqs int64[k], req_digests uint8[k, 32])."""
+        n = cols.n
+        nb = (n + 7) // 8 + 1
+        out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
+        sbm = np.zeros(nb, np.uint8) if sigs is not None else None
+        mbm = np.zeros(nb, np.uint8) if states is not None else None
+        sp = kp = svp = slp = sdp = sip = None
+        k = 0
+        if sigs is not None:
+            sigs = np.ascontiguousarray(sigs, np.uint8)
+            key_idx = np.ascontiguousarray(key_idx, np.uint32)
+            sp, kp = sigs.ctypes.data, key_idx.ctypes.data
+        if states is not None:
+            sv = np.ascontiguousarray(states[0], np.int64)
+            sl = np.ascontiguousarray(states[1], np.int64)
+            sd = np.ascontiguousarray(states[2], np.uint8)
+            si = np.ascontiguousarray(state_idx, np.uint32)
+            k = len(sv)
+            svp, slp, sdp, sip = sv.ctypes.data, sl.ctypes.data, sd.ctypes.data, si.ctypes.data
+        _check(self._L.pbftv_flush_votes(self._h, n, *cols.args(), sp, kp, k, svp, slp, sdp, sip,
+                                         _ptr(out_d), _ptr(sbm), _ptr(mbm)))
+        return (out_d[:n] if digests else None, bitmap_to_bool(sbm, n) if sbm is not None else None,
+                bitmap_to_bool(mbm, n) if mbm is not None else None)
 
     # ---- ecdsa
     def register_keys(self, pub_xy: np.ndarray) -> np.ndarray:

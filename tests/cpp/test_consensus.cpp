@@ -363,6 +363,115 @@ static void test_pools() {
   CHECK(rq.MsgNum() == 1);
 }
 
+// Sequence-keyed consensus: K sequences in flight at one replica, every prepare
+// and commit of all of them in ONE flush each (ConsensusTable), against the
+// reference's one-state-at-a-time flush (State::PrepareBatch / CommitBatch) run
+// per sequence over the same votes in the same order.
+static void test_concurrent_sequences(Crypto& c) {
+  Cluster cl(c);
+  const int K = 40;
+  const int64_t seq0 = 1668519247222762700;
+  ConsensusTable tab(kView);
+  std::vector<State> ref;
+  std::vector<std::string> dg(K);
+  for (int k = 0; k < K; ++k) {
+    RequestMsg r;
+    r.Timestamp = 1668519246 + k;
+    r.ClientID = "client" + std::to_string(k % 3 + 1);
+    r.Operation = k % 4 ? "printf" : "a<b>&\"c\"\n";  // HTML / escapes in the preimage
+    RequestMsg r2 = r;
+    auto pp = tab.Open(seq0 + k).StartConsensus(c, r, seq0 + k);
+    ref.push_back(State::CreateState(kView, -1));
+    auto pr = ref.back().StartConsensus(c, r2, seq0 + k);
+    CHECK(pp.value && pr.value && pp.value->SequenceID == seq0 + k && pp.value->Digest == pr.value->Digest);
+    dg[k] = pp.value->Digest;
+  }
+  CHECK(tab.Size() == (size_t)K);
+  // prepares from ReplicaNode1..3 for every sequence, with faults:
+  //   k % 5 == 1: ReplicaNode1's signature flipped;  k % 7 == 2: ReplicaNode2 votes an upper-case digest;
+  //   k % 6 == 3: ReplicaNode3 votes the wrong view; k % 9 == 4: ReplicaNode1 AND ReplicaNode2 bad (no quorum)
+  SeqVotePool pool;
+  for (int k = 0; k < K; ++k)
+    for (int r = 1; r < 4; ++r) {
+      VoteMsg v;
+      v.ViewID = kView;
+      v.SequenceID = seq0 + k;
+      v.Digest = dg[k];
+      v.NodeID = kNames[r];
+      v.Type = PrepareMsg;
+      if (r == 2 && (k % 7 == 2 || k % 9 == 4))
+        for (auto& ch : v.Digest) ch = (char)toupper(ch);
+      if (r == 3 && k % 6 == 3) v.ViewID = kView + 1;
+      cl.sign(v, cl.nodes[r].key);
+      if (r == 1 && (k % 5 == 1 || k % 9 == 4)) v.Signature[7] ^= 0x10;
+      pool.Add(v);
+    }
+  VoteMsg stray;  // a vote for a sequence this replica has no state for
+  stray.ViewID = kView;
+  stray.SequenceID = seq0 - 1;
+  stray.Digest = dg[0];
+  stray.NodeID = kNames[1];
+  cl.sign(stray, cl.nodes[1].key);
+  pool.Add(stray);
+  const auto snap = pool.GetAll();
+  CHECK(snap.size() == (size_t)(3 * K + 1));
+  auto o = tab.FlushPrepares(c, cl.keys, snap);
+  CHECK(o.accepted.size() == snap.size());
+  int prepared = 0;
+  for (int k = 0; k < K; ++k) {
+    std::vector<VoteMsg> sub;
+    std::vector<size_t> where;
+    for (size_t i = 0; i < snap.size(); ++i)
+      if (snap[i].SequenceID == seq0 + k) {
+        sub.push_back(snap[i]);
+        where.push_back(i);
+      }
+    BatchOutcome ro;
+    auto cv = ref[k].PrepareBatch(c, cl.keys, sub, &ro);
+    for (size_t j = 0; j < sub.size(); ++j) {
+      CHECK(o.accepted[where[j]] == ro.accepted[j]);
+      CHECK(o.errors[where[j]] == ro.errors[j]);
+    }
+    State* s = tab.Find(seq0 + k);
+    CHECK(s && s->CurrentStage == ref[k].CurrentStage);
+    CHECK(s && s->MsgLogs_.PrepareMsgs.size() == ref[k].MsgLogs_.PrepareMsgs.size());
+    const bool want = !(k % 9 == 4) && !((k % 5 == 1) + (k % 7 == 2) + (k % 6 == 3) >= 2);
+    CHECK((ref[k].CurrentStage == Stage::Prepared) == want);
+    prepared += cv.value.has_value();
+  }
+  for (size_t i = 0; i < snap.size(); ++i)
+    if (snap[i].SequenceID == seq0 - 1) CHECK(!o.accepted[i] && o.errors[i] == "prepare message is corrupted");
+  CHECK((int)o.commits.size() == prepared && prepared > K / 2 && prepared < K);
+  // commits from all four nodes for the prepared sequences; MainNode's commit bad on k % 4 == 0
+  SeqVotePool cpool;
+  for (const auto& cv : o.commits)
+    for (int r = 0; r < 4; ++r) {
+      VoteMsg v = cv;
+      v.NodeID = kNames[r];
+      cl.sign(v, cl.nodes[r].key);
+      if (r == 0 && (v.SequenceID - seq0) % 4 == 0) v.Signature[20] ^= 0x01;
+      cpool.Add(v);
+    }
+  const auto csnap = cpool.GetAll();
+  auto co = tab.FlushCommits(c, cl.keys, csnap);
+  CHECK((int)co.replies.size() == prepared);
+  int64_t last = -1;
+  for (int k = 0; k < K; ++k) {
+    if (ref[k].CurrentStage != Stage::Prepared) continue;
+    std::vector<VoteMsg> sub;
+    for (const auto& v : csnap)
+      if (v.SequenceID == seq0 + k) sub.push_back(v);
+    auto rr = ref[k].CommitBatch(c, cl.keys, sub);
+    State* s = tab.Find(seq0 + k);
+    CHECK(rr.value && s && s->CurrentStage == Stage::Committed && ref[k].CurrentStage == Stage::Committed);
+    CHECK(s && s->LastSequenceID == seq0 + k && s->MsgLogs_.CommitMsgs.size() == ref[k].MsgLogs_.CommitMsgs.size());
+    last = seq0 + k;
+  }
+  CHECK(tab.LastCommitted() == last);
+  // a state opened now starts after the highest committed sequence (createStateForNewConsensus)
+  CHECK(tab.Open(seq0 + 1000).LastSequenceID == last);
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "oracle";
   std::unique_ptr<Crypto> c;
@@ -379,6 +488,7 @@ int main(int argc, char** argv) {
   test_pools();
   test_verifymsg_semantics(*c);
   test_logged_run(*c);
+  test_concurrent_sequences(*c);
   std::printf("%s: %d checks passed, %d failed\n", mode.c_str(), g_pass, g_fail);
   return g_fail ? 1 : 0;
 }
