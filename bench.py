@@ -50,15 +50,28 @@ JADD = 12 * FE_MUL + 4 * FE_SQR                    # add-2007-bl (final complete
 CHECK = 2 * FE_MUL                                  # X == r ZZ test: r to Montgomery form, r ZZ
 
 
+def window_widths(code: int) -> list:
+    """Window widths of a comb geometry code (p256_algo.h CombGeom): W-bit
+    windows, or the mixed codes splitting 257 bits into wide bottom windows and
+    one-bit-narrower top ones (21: 5 x 22 + 7 x 21, 29: 5 x 29 + 4 x 28)."""
+    mixed = {11: (12, 22), 21: (22, 12), 29: (29, 9)}
+    if code in mixed:
+        kw, nwin = mixed[code]
+        low = nwin * kw - 257
+        return [kw] * (nwin - low) + [kw - 1] * low
+    return [code] * (256 // code + 1)
+
+
 def macs_comb(gbits: int, qbits: int) -> float:
     """Joint comb (p256_kernels.hip k_ecdsa_comb): one mixed addition per nonzero
     signed digit of u1 (G table) and u2 (key table), minus the first (a load).
     Windows below 256 bits are nonzero w.p. 1 - 2^-W; the top (carry) window
     w.p. ~1/2 when 256 % W == 0, else its 256 % W real bits make it nonzero."""
     def nonzero(w):
-        full = 256 // w
-        top = 0.5 if 256 % w == 0 else 1.0
-        return full * (1 - 2.0 ** -w) + top
+        ws = window_widths(w)
+        top_bits = 256 - sum(ws[:-1])
+        top = 0.5 if top_bits <= 0 else 1.0
+        return sum(1 - 2.0 ** -x for x in ws[:-1]) + top
     return (nonzero(gbits) + nonzero(qbits) - 1) * MADD + CHECK
 
 
@@ -314,8 +327,8 @@ VALU_PEAK = 256 * 4 * 32 * 2.4e9   # full-rate 32-bit VALU: 256 CU x 4 SIMD x 32
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=1 << 20, help="signatures per rank")
     ap.add_argument("--keys", type=int, default=100)
     ap.add_argument("--no-extras", action="store_true", help="skip QC latency and CPU baseline")
@@ -335,6 +348,12 @@ def main():
     ver = Verifier(device_mask=1 if share else 1 << local)
     n = args.n
     pub, H, S, K, ok = synth.config4(n, n_keys=args.keys, seed=0x50424654 + rank)
+    sk = int(os.environ.get("PBFTV_EXP_SORT_KEYS", "0"))
+    if sk:  # experiment only: batch pre-sorted by key (1: whole batch, c: within chunks of c) -- not a bench line
+        c = n if sk == 1 else sk
+        o = (np.arange(n) // c).astype(np.int64) * (1 << 32) + K
+        o = np.argsort(o, kind="stable")
+        H, S, K, ok = H[o], S[o], K[o], ok[o]
     valid = ver.register_keys(pub)
     assert valid.all()
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
@@ -395,9 +414,11 @@ def main():
         ach = kern[dom]["achieved_tmacs"]
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc):  # PMC passes of the same workload (tools/pmc_passes.sh), same table geometry only
             with open(pmc) as f:
-                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+                pm = json.load(f)
+            if pm.get("ecdsa_comb", {}).get("geometry") == [gb, qb]:
+                traffic = pm.get(dom, {}).get("hbm_bytes_per_launch")
         out["roofline"] = {"bound": "valu", "kernel": dom, "achieved": ach, "peak": MAD_PEAK / 1e12,
                            "unit": "TMAC/s (v_mad_u64_u32 limb MACs)", "frac": ach * 1e12 / MAD_PEAK,
                            "traffic": traffic}

@@ -32,9 +32,11 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define PBFTV_HD __host__ __device__ __forceinline__
+#define PBFTV_HDM __host__ __device__  // member functions
 #define PBFTV_UNROLL _Pragma("unroll")
 #else
 #define PBFTV_HD static inline
+#define PBFTV_HDM
 #define PBFTV_UNROLL
 #endif
 

@@ -7,9 +7,16 @@
 namespace pbftv {
 
 // ---- ECDSA-P256 (p256_kernels.hip) ----
-// Comb tables: W-bit signed windows, W in {8, 12, 16}; table_bytes(W) per base
-// (8: 264 KiB, 12: 2.75 MiB, 16: 34 MiB).
+// Comb tables: geometry code w (p256_algo.h CombGeom: W-bit windows, or the
+// mixed 21 / 29); table_bytes(w) per base (8: 264 KiB, 16: 34 MiB, 21:
+// 1.14 GB, 22: 1.61 GB, 24: 5.9 GB, 26: 21.5 GB, 29: 120 GB).
 size_t table_bytes(int w);
+int table_windows(int w);  // windows = table entries added per scalar
+// (G, key) geometry pairs with instantiated verify kernels
+#define PBFTV_COMBOS(X)                                                                                       \
+  X(29, 24) X(29, 22) X(29, 21) X(29, 20) X(29, 16) X(26, 24) X(26, 22) X(26, 21) X(26, 20) X(26, 16)          \
+  X(24, 24) X(24, 22) X(24, 20) X(20, 20) X(24, 16) X(16, 16) X(16, 12) X(16, 8) X(8, 8)
+#define PBFTV_TABLE_WIDTHS(X) X(8) X(12) X(16) X(20) X(21) X(22) X(24) X(26) X(29)
 struct TableScratch {
   void* bases;
   void* lbuf;
@@ -34,12 +41,19 @@ int scalar_batch(uint64_t n);
 size_t scalar_prefix_bytes(uint64_t n);
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                                 const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, void* prefix,
-                                hipStream_t st);
-// stage 2: (wg, wq) in {(16,16), (16,12), (16,8), (8,8)}; qtabs = nkeys tables of width wq;
+                                const uint32_t* perm, hipStream_t st);
+// stage 2: (wg, wq) one of PBFTV_COMBOS; qtabs = nkeys tables of width wq;
 // bitmap ceil(n/8) B
 hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* flag, const uint8_t* sigs,
                              const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
-                             uint8_t* bitmap, hipStream_t st);
+                             uint8_t* bitmap, const uint32_t* perm, uint8_t* okb, hipStream_t st);
+// stage 0 (optional): key order perm[p] = signature at position p sorted by key
+// (scratch: key_sort_scratch_bytes, perm first); with a perm the comb writes
+// okb[i] (n B) and launch_pack_bits builds the bitmap.
+bool key_sort_wanted(uint64_t n, uint32_t nkeys);
+size_t key_sort_scratch_bytes(uint64_t n, uint32_t nkeys);
+hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, hipStream_t st);
+hipError_t launch_pack_bits(const uint8_t* okb, uint64_t n, uint8_t* bitmap, hipStream_t st);
 // latency path for small batches: one wave per signature (scalars, per-window
 // points, butterfly sum, check) in one launch.  Output: okbytes[i] (one byte per
 // signature) when okbytes != nullptr, else bit i of bitmap set/cleared by word

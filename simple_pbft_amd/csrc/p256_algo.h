@@ -27,15 +27,39 @@ namespace pbftv {
 // Comb table geometry for W-bit signed windows: digits d_i in
 // [-(2^(W-1) - 1), 2^(W-1)], u = sum d_i 2^(W i); entry (i, |d|-1) holds
 // |d| * 2^(W i) * B as affine (x, y), canonical Montgomery-form, 8+8 LE words.
+//
+// Geometry codes: W <= 26 is W-bit windows throughout.  The MIXED codes split
+// exactly 257 bits (the least that absorbs the last recoding carry) into kWin
+// windows, the bottom kWin - kLow of kW bits and the top kLow of kW - 1 bits:
+//   11: 15 x 12 + 7 x 11  (22 windows; CPU harness)
+//   21:  5 x 22 + 7 x 21  (12 windows, 1.14 GB per key instead of 1.61 at W = 22)
+//   29:  5 x 29 + 4 x 28  ( 9 windows, 120 GB -- one window fewer than W = 26)
+// A narrower top window holds 2^(kW-2) entries; its digit still fits, since
+// the bits left for it number its width - 1.
+constexpr bool comb_mixed(int c) { return c == 11 || c == 21 || c == 29; }
+constexpr int comb_kw(int c) { return c == 11 ? 12 : c == 21 ? 22 : c; }
+constexpr int comb_win(int c) { return c == 11 ? 22 : c == 21 ? 12 : c == 29 ? 9 : 256 / c + 1; }
+
 template <int W>
 struct CombGeom {
-  static_assert(W >= 8 && W <= 26, "window width");
-  static_assert(256 % W <= W - 2, "top window must absorb the recoding carry");
-  static constexpr int kW = W;
-  static constexpr int kWin = 256 / W + 1;  // 33 (W=8), 22 (12), 17 (16), 13 (20), 12 (22), 11 (24), 10 (26)
-  static constexpr int kEnt = 1 << (W - 1);
-  static constexpr uint64_t kWords = (uint64_t)kWin * kEnt * 16;
+  static constexpr int kCode = W;
+  static constexpr int kW = comb_kw(W);
+  static constexpr int kWin = comb_win(W);  // 33 (W=8), 22 (12), 17 (16), 13 (20), 12 (22), 11 (24), 10 (26), 9 (29)
+  static constexpr int kLow = comb_mixed(W) ? kWin * kW - 257 : 0;
+  static constexpr int kHi = kWin - kLow;
+  static_assert(kW >= 8 && kW <= 29, "window width");
+  static_assert(comb_mixed(W) ? kLow > 0 && kLow < kWin : 256 % W <= W - 2,
+                "top window must absorb the recoding carry");
+  static constexpr int kEnt = 1 << (kW - 1);  // entries of a full-width window
+  static constexpr uint64_t kWords = ((uint64_t)kHi * kEnt + (uint64_t)kLow * (kEnt / 2)) * 16;
   static constexpr uint64_t kBytes = kWords * 4;
+  PBFTV_HDM static constexpr int width(int i) { return i < kHi ? kW : kW - 1; }
+  PBFTV_HDM static constexpr int bit(int i) { return i < kHi ? i * kW : kHi * kW + (i - kHi) * (kW - 1); }
+  PBFTV_HDM static constexpr int ent(int i) { return i < kHi ? kEnt : kEnt / 2; }
+  // first entry of window i
+  PBFTV_HDM static constexpr uint64_t base(int i) {
+    return i < kHi ? (uint64_t)i * kEnt : (uint64_t)kHi * kEnt + (uint64_t)(i - kHi) * (kEnt / 2);
+  }
 };
 
 // legacy names for the W = 8 geometry
@@ -307,17 +331,17 @@ PBFTV_HD bool ecdsa_scalars(const uint32_t e_w[8], const uint32_t r_w[8], const 
 // digit i of u (LE words), carry-in c (0/1); returns d in [-(2^(W-1)-1), 2^(W-1)], updates c.
 template <int W>
 PBFTV_HD int signed_digit_w(const uint32_t u_w[8], int i, int& c) {
-  const int bit = W * i;
+  const int bit = CombGeom<W>::bit(i), wd = CombGeom<W>::width(i);
   uint32_t b = 0;
   if (bit < 256) {
     const int wi = bit >> 5, sh = bit & 31;
     uint64_t two = u_w[wi];
     if (wi + 1 < 8) two |= (uint64_t)u_w[wi + 1] << 32;
-    b = (uint32_t)(two >> sh) & ((1u << W) - 1u);
+    b = (uint32_t)(two >> sh) & ((1u << wd) - 1u);
   }
   const int d = (int)b + c;
-  c = d > (1 << (W - 1)) ? 1 : 0;
-  return d - (c << W);
+  c = d > (1 << (wd - 1)) ? 1 : 0;
+  return d - (c << wd);
 }
 
 PBFTV_HD int signed_digit(const uint32_t u_w[8], int i, int& c) { return signed_digit_w<8>(u_w, i, c); }
@@ -710,11 +734,11 @@ PBFTV_HD void build_table_serial(uint32_t* table, const fe& bx, const fe& by, ui
   constexpr int NH = G::kEnt / CL;
   for (int win = 0; win < G::kWin; ++win) {
     uint32_t bw[16];
-    window_base(bw, W * win, bx, by);
+    window_base(bw, G::bit(win), bx, by);
     multiples(lbuf, CL, bw, st, ld);
     if (NH > 1) multiples(hbuf, NH - 1, lbuf + (uint64_t)(CL - 1) * 16, st, ld);
-    uint32_t* tw = table + (uint64_t)win * G::kEnt * 16;
-    for (int hi = 0; hi < NH; ++hi)
+    uint32_t* tw = table + G::base(win) * 16;
+    for (int hi = 0; hi < G::ent(win) / CL; ++hi)
       sums_chunk(tw + (uint64_t)hi * CL * 16, CL, hi > 0, hbuf + (uint64_t)(hi > 0 ? hi - 1 : 0) * 16, lbuf, st, ld);
   }
 }

@@ -28,6 +28,10 @@ namespace pbftv {
 #define PBFTV_COMB_WAVES 4  // min waves per SIMD for k_ecdsa_comb: 128 VGPRs; +1.2 % over 2 (tools/ab.sh)
 #endif
 
+// key-order sort (k_key_*): blocks of the histogram/scatter passes, largest key count sorted
+constexpr uint32_t kSortBlocks = 256;
+constexpr uint32_t kSortMaxKeys = 1024;
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // 32 big-endian bytes at p (16-B aligned) -> 8 LE words
@@ -49,7 +53,7 @@ struct TabGeom {
   // W = 16 CL = 256; wider windows split E = CL * NH near sqrt(E) so neither
   // phase-2 walk gets long (W = 20: 1024 x 512, W = 24: 4096 x 2048,
   // W = 26: 8192 x 4096).
-  static constexpr int CL = G::kEnt < 256 ? G::kEnt : (W <= 16 ? 256 : 1 << (W / 2));
+  static constexpr int CL = G::kEnt < 256 ? G::kEnt : (G::kW <= 16 ? 256 : 1 << (G::kW / 2));
   static constexpr int NH = G::kEnt / CL;
   static constexpr int PC = CL < 64 ? CL : 64;              // entries per phase-3 lane
   static constexpr int SS = 4 * (CL > NH - 1 ? CL : NH - 1);  // phase-2 scratch slots per lane
@@ -83,7 +87,7 @@ __global__ void __launch_bounds__(64) k_tab_bases(const uint32_t* __restrict__ k
   fe bx, by;
   const bool ok = load_base(keys_le, key0, b, with_g, bx, by);
   if (win == 0 && !(with_g && b == 0)) valid[key0 + b - with_g] = ok ? 1u : 0u;
-  window_base(bases + (uint64_t)lane * 16, W * (int)win, bx, by);
+  window_base(bases + (uint64_t)lane * 16, CombGeom<W>::bit((int)win), bx, by);
 }
 
 // phase 2: lane (b, win) -> L = (lo+1) B_i (CL points) and H = hi (CL B_i) (NH-1 points)
@@ -128,12 +132,13 @@ __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__
   const uint32_t win = rem / (T::NH * parts);
   rem %= T::NH * parts;
   const uint32_t hi = rem / parts, part = rem % parts;
+  if ((uint64_t)hi * T::CL >= (uint64_t)G::ent((int)win)) return;  // narrow top window: half the entries
   const uint64_t bw = (uint64_t)b * G::kWin + win;  // (base, window) index into lbuf/hbuf
   const uint32_t* L = lbuf + (bw * T::CL + (uint64_t)part * T::PC) * 16;
   uint32_t hw[16] = {0};
   if (hi > 0)
     for (int i = 0; i < 16; ++i) hw[i] = hbuf[(bw * (T::NH - 1) + hi - 1) * 16 + i];
-  uint32_t* out = tables + (uint64_t)b * G::kWords + ((uint64_t)win * G::kEnt + (uint64_t)hi * T::CL +
+  uint32_t* out = tables + (uint64_t)b * G::kWords + (G::base((int)win) + (uint64_t)hi * T::CL +
                                                       (uint64_t)part * T::PC) * 16;
   fe* sc = scratch + local * 4 * T::PC;
   sums_chunk(out, T::PC, hi > 0, hw, L, [&](int slot, const fe& v) { sc[slot] = v; },
@@ -168,7 +173,7 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
   TableScratchSizes z{};
   auto fill = [&](auto geom) {
     using G = decltype(geom);
-    using T = TabGeom<G::kW>;
+    using T = TabGeom<G::kCode>;
     z.bases = (size_t)nb * G::kWin * 64;
     z.lbuf = (size_t)nb * G::kWin * T::CL * 64;
     z.hbuf = (size_t)nb * G::kWin * (T::NH > 1 ? T::NH - 1 : 1) * 64;
@@ -179,12 +184,10 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
     z.entry_scratch = (size_t)z.entry_lanes * 4 * T::PC * sizeof(fe);
   };
   switch (w) {
-    case 8: fill(CombGeom<8>()); break;
-    case 12: fill(CombGeom<12>()); break;
-    case 16: fill(CombGeom<16>()); break;
-    case 20: fill(CombGeom<20>()); break;
-    case 22: fill(CombGeom<22>()); break;
-    case 26: fill(CombGeom<26>()); break;
+#define PBFTV_W(W) \
+  case W: fill(CombGeom<W>()); break;
+    PBFTV_TABLE_WIDTHS(PBFTV_W)
+#undef PBFTV_W
     default: fill(CombGeom<24>()); break;
   }
   return z;
@@ -192,13 +195,20 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
 
 size_t table_bytes(int w) {
   switch (w) {
-    case 8: return CombGeom<8>::kBytes;
-    case 12: return CombGeom<12>::kBytes;
-    case 16: return CombGeom<16>::kBytes;
-    case 20: return CombGeom<20>::kBytes;
-    case 22: return CombGeom<22>::kBytes;
-    case 24: return CombGeom<24>::kBytes;
-    case 26: return CombGeom<26>::kBytes;
+#define PBFTV_W(W) \
+  case W: return CombGeom<W>::kBytes;
+    PBFTV_TABLE_WIDTHS(PBFTV_W)
+#undef PBFTV_W
+    default: return 0;
+  }
+}
+
+int table_windows(int w) {
+  switch (w) {
+#define PBFTV_W(W) \
+  case W: return CombGeom<W>::kWin;
+    PBFTV_TABLE_WIDTHS(PBFTV_W)
+#undef PBFTV_W
     default: return 0;
   }
 }
@@ -206,13 +216,10 @@ size_t table_bytes(int w) {
 hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g,
                                uint32_t* valid, uint32_t* tables, TableScratch& sc, hipStream_t st) {
   switch (w) {
-    case 8: return build_tables_w<8>(keys_le, key0, nb, with_g, valid, tables, sc, st);
-    case 12: return build_tables_w<12>(keys_le, key0, nb, with_g, valid, tables, sc, st);
-    case 16: return build_tables_w<16>(keys_le, key0, nb, with_g, valid, tables, sc, st);
-    case 20: return build_tables_w<20>(keys_le, key0, nb, with_g, valid, tables, sc, st);
-    case 22: return build_tables_w<22>(keys_le, key0, nb, with_g, valid, tables, sc, st);
-    case 24: return build_tables_w<24>(keys_le, key0, nb, with_g, valid, tables, sc, st);
-    case 26: return build_tables_w<26>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+#define PBFTV_W(W) \
+  case W: return build_tables_w<W>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+    PBFTV_TABLE_WIDTHS(PBFTV_W)
+#undef PBFTV_W
     default: return hipErrorInvalidValue;
   }
 }
@@ -244,7 +251,10 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
                                                        const uint32_t* __restrict__ key_idx, uint64_t n,
                                                        const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                        uint4* __restrict__ scal, uint8_t* __restrict__ flag,
-                                                       uint32_t* __restrict__ prefix) {
+                                                       uint32_t* __restrict__ prefix,
+                                                       const uint32_t* __restrict__ perm) {
+  // outputs at position i; inputs of signature src(i) = perm[i] in key order (k_key_*)
+  auto src = [&](uint64_t i) -> uint64_t { return perm != nullptr ? (uint64_t)perm[i] : i; };
   const uint64_t L = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   fe r2n, acc;
@@ -257,7 +267,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     bool ok = false;
     if (i < n) {
       uint32_t s[8];
-      ok = sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s);
+      ok = sig_ok(sigs, key_idx, key_valid, nkeys, src(i), r, s);
       if (ok) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
     }
     fe sv, sm;
@@ -274,9 +284,10 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     const uint64_t i = lane + (uint64_t)j * L;
     const bool ok = (okm >> j) & 1u;
     uint32_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t si = ok ? src(i) : 0;
     if (ok) {
-      load_be256(sigs + 64 * i, r);
-      load_be256(sigs + 64 * i + 32, s);
+      load_be256(sigs + 64 * si, r);
+      load_be256(sigs + 64 * si + 32, s);
     }
     fe w;
     if (K > 1 && j > 0) {
@@ -294,7 +305,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
       uint32_t u1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, u2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       if (ok) {
         uint32_t e[8];
-        load_be256(hashes + 32 * i, e);
+        load_be256(hashes + 32 * si, e);
         fe ev, rv, t;
         fe_from_words(ev, e);
         fe_from_words(rv, r);
@@ -323,13 +334,15 @@ template <int W>
 struct digit_stream {
   uint32_t w[8];
   int carry;
+  int k = 0;  // next window (its width differs only in the mixed geometries)
   __device__ __forceinline__ int next() {
-    const int b = (int)(w[0] & ((1u << W) - 1u));
-    PBFTV_UNROLL for (int j = 0; j < 7; ++j) w[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], W);
-    w[7] >>= W;
+    const int wd = CombGeom<W>::width(k++);
+    const int b = (int)(w[0] & ((1u << wd) - 1u));
+    PBFTV_UNROLL for (int j = 0; j < 7; ++j) w[j] = __builtin_amdgcn_alignbit(w[j + 1], w[j], wd);
+    w[7] >>= wd;
     const int d = b + carry;
-    carry = d > (1 << (W - 1)) ? 1 : 0;
-    return d - (carry << W);
+    carry = d > (1 << (wd - 1)) ? 1 : 0;
+    return d - (carry << wd);
   }
 };
 
@@ -337,9 +350,9 @@ template <int W>
 __device__ __forceinline__ void load_entry(const uint4* __restrict__ tab, int win, int d, uint4 e[4]) {
   const int idx = (d < 0 ? -d : d) - 1;
 #ifdef PBFTV_EXP_L2TAB  // timing experiment only: lookups confined to 4 MiB per window (results wrong)
-  const uint4* p = tab + ((uint64_t)win * CombGeom<W>::kEnt + (idx < 0 ? 0 : idx & 0xFFFF)) * 4;
+  const uint4* p = tab + (CombGeom<W>::base(win) + (idx < 0 ? 0 : idx & 0xFFFF)) * 4;
 #else
-  const uint4* p = tab + ((uint64_t)win * CombGeom<W>::kEnt + (idx < 0 ? 0 : idx)) * 4;
+  const uint4* p = tab + (CombGeom<W>::base(win) + (idx < 0 ? 0 : idx)) * 4;
 #endif
   e[0] = p[0]; e[1] = p[1]; e[2] = p[2]; e[3] = p[3];
 }
@@ -419,7 +432,7 @@ struct CombSteps {
   static constexpr int nMin = nG < nQ ? nG : nQ;
   static constexpr int nD = nG + nQ;
   // LDS digit storage: d - 1 fits int16 for W <= 16 (d in [-(2^15 - 1), 2^15])
-  using Digit = std::conditional_t<(WG > 16 || WQ > 16), int, short>;
+  using Digit = std::conditional_t<(CombGeom<WG>::kW > 16 || CombGeom<WQ>::kW > 16), int, short>;
   __host__ __device__ static constexpr bool is_q(int j) { return j < 2 * nMin ? (j & 1) != 0 : nQ > nG; }
   __host__ __device__ static constexpr int win(int j) { return j < 2 * nMin ? j >> 1 : j - nMin; }
 };
@@ -437,7 +450,7 @@ __device__ __forceinline__ const uint4* entry_ptr(const uint4* __restrict__ tab,
 #ifdef PBFTV_EXP_SMALLTAB  // timing experiment only: 256 KiB footprint per table (results wrong)
   return tab + (uint64_t)(idx < 0 ? 0 : idx & 0xFFF) * 4;
 #else
-  return tab + ((uint64_t)win * CombGeom<W>::kEnt + (idx < 0 ? 0 : idx)) * 4;
+  return tab + (CombGeom<W>::base(win) + (idx < 0 ? 0 : idx)) * 4;
 #endif
 }
 
@@ -466,7 +479,9 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint
                                                        const uint32_t* __restrict__ key_idx, uint64_t n,
                                                        const uint4* __restrict__ gtab,
                                                        const uint4* __restrict__ qtabs,
-                                                       uint8_t* __restrict__ bitmap) {
+                                                       uint8_t* __restrict__ bitmap,
+                                                       const uint32_t* __restrict__ perm,
+                                                       uint8_t* __restrict__ okb) {
   using S = CombSteps<WG, WQ>;
   // signed digits of u1 / u2 in step order, one column per thread: recoded once
   // in the prologue so the main loop holds no 256-bit digit shift registers
@@ -475,11 +490,13 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint
   // while it is in flight): piece k of thread t at sent[k][t]
   __shared__ uint4 sent[4][256];
   const uint32_t t = threadIdx.x;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + t;
-  const bool active = i < n && flag[i];
+  // lane position p; with a key order (k_key_*), p is the p-th signature by key
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + t;
+  const uint64_t i = perm != nullptr && p < n ? (uint64_t)perm[p] : p;
+  const bool active = p < n && flag[p];  // stage 1 wrote scal/flag in the same (key) order
   bool ok = false;
   if (active) {
-    const uint4* sp = scal + 4 * i;
+    const uint4* sp = scal + 4 * p;
     {
       const uint4 a = sp[0], b = sp[1], c = sp[2], dd = sp[3];
       digit_stream<WG> s1;
@@ -542,11 +559,128 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint
       ok = ecdsa_check(R, !inf, r);
     }
   }
+  if (perm != nullptr) {  // key order: one byte per signature, k_pack_bits builds the bitmap
+    if (p < n) okb[i] = ok ? 1 : 0;
+    return;
+  }
   // LSB-first bitmap: wave ballot, lanes 0..7 store one byte each
   const unsigned long long m = __ballot(ok);
   const uint32_t lane = t & 63u;
-  const uint64_t wave_base = i - lane;
+  const uint64_t wave_base = p - lane;
   if (lane < 8 && wave_base + 8 * lane < n) bitmap[(wave_base >> 3) + lane] = (uint8_t)(m >> (8 * lane));
+}
+
+// ---------------------------------------------------------------------------
+// Key order for the comb (stage 0).  The key tables are looked up at random
+// entries; when the 64 lanes of a wave name ~50 different keys (a random
+// 100-key batch) every wave-wide table load touches ~50 tables, when they
+// share a key the lookups fall in one table window like the G lookups do.
+// Same-box A/B at 1M signatures / 100 keys (bench.py PBFTV_EXP_SORT_KEYS): comb
+// 1.345 ms in arrival order, 1.237 ms key-sorted.  A counting sort in three
+// small launches: per-block key histograms in LDS added into per-key totals ->
+// exclusive scan of the totals -> each block claims its range of every key
+// with one atomic per (block, key) and scatters through LDS cursors.  Not
+// stable (the order inside a key does not matter: results go back to the
+// signature's own index).
+__device__ __forceinline__ void block_key_hist(uint32_t* h, const uint32_t* __restrict__ key_idx, uint64_t n,
+                                               uint32_t nkeys) {
+  const uint32_t nb = nkeys + 1;  // bin nkeys: out-of-range key indices (rejected later)
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = (uint64_t)blockIdx.x * chunk;
+  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t k = key_idx[i];
+    atomicAdd(&h[k < nkeys ? k : nkeys], 1u);
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_key_hist(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
+                                                  uint32_t* __restrict__ total) {
+  __shared__ uint32_t h[kSortMaxKeys + 1];
+  block_key_hist(h, key_idx, n, nkeys);
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
+    if (h[b]) atomicAdd(&total[b], h[b]);
+}
+
+// exclusive scan of the m <= 2048 totals in place: one block, two per thread
+__global__ void __launch_bounds__(1024) k_key_scan(uint32_t* __restrict__ total, uint32_t m) {
+  __shared__ uint32_t s[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t a = 2 * t < m ? total[2 * t] : 0u, b = 2 * t + 1 < m ? total[2 * t + 1] : 0u;
+  s[t] = a + b;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    const uint32_t v = t >= off ? s[t - off] : 0u;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  const uint32_t excl = s[t] - a - b;
+  if (2 * t < m) total[2 * t] = excl;
+  if (2 * t + 1 < m) total[2 * t + 1] = excl + a;
+}
+
+__global__ void __launch_bounds__(256) k_key_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
+                                                     uint32_t* __restrict__ start, uint32_t* __restrict__ perm) {
+  __shared__ uint32_t h[kSortMaxKeys + 1];
+  block_key_hist(h, key_idx, n, nkeys);
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
+    if (h[b]) h[b] = atomicAdd(&start[b], h[b]);  // this block's range of key b
+  __syncthreads();
+  const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = (uint64_t)blockIdx.x * chunk;
+  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t k = key_idx[i];
+    perm[atomicAdd(&h[k < nkeys ? k : nkeys], 1u)] = (uint32_t)i;
+  }
+}
+
+// LSB-first bitmap from one byte per signature
+__global__ void __launch_bounds__(256) k_pack_bits(const uint8_t* __restrict__ okb, uint64_t n,
+                                                   uint8_t* __restrict__ bitmap) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (8 * b >= n) return;
+  uint32_t v = 0;
+  if (8 * b + 8 <= n) {
+    const uint2 w = *reinterpret_cast<const uint2*>(okb + 8 * b);
+    PBFTV_UNROLL for (int k = 0; k < 4; ++k) v |= ((w.x >> (8 * k)) & 1u) << k;
+    PBFTV_UNROLL for (int k = 0; k < 4; ++k) v |= ((w.y >> (8 * k)) & 1u) << (4 + k);
+  } else {
+    for (uint64_t k = 0; 8 * b + k < n; ++k) v |= (okb[8 * b + k] ? 1u : 0u) << k;
+  }
+  bitmap[b] = (uint8_t)v;
+}
+
+bool key_sort_wanted(uint64_t n, uint32_t nkeys) {
+  if (const char* e = getenv("PBFTV_KEY_SORT")) {
+    if (e[0] == '0') return false;
+    if (e[0] == '1') return nkeys <= kSortMaxKeys && n < (1ull << 32);
+  }
+  return nkeys > 8 && nkeys <= kSortMaxKeys && n >= 32768 && n < (1ull << 32);
+}
+
+size_t key_sort_scratch_bytes(uint64_t n, uint32_t nkeys) { return (size_t)n * 4 + (size_t)(nkeys + 1) * 4; }
+
+hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (nkeys > kSortMaxKeys) return hipErrorInvalidValue;
+  uint32_t* perm = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* total = perm + n;
+  hipError_t e = hipMemsetAsync(total, 0, (size_t)(nkeys + 1) * 4, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_key_hist, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, total);
+  hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(1024), 0, st, total, nkeys + 1);
+  hipLaunchKernelGGL(k_key_scatter, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, total, perm);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_bits(const uint8_t* okb, uint64_t n, uint8_t* bitmap, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint64_t bytes = (n + 7) / 8;
+  hipLaunchKernelGGL(k_pack_bits, dim3((uint32_t)((bytes + 255) / 256)), dim3(256), 0, st, okb, n, bitmap);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -884,23 +1018,14 @@ hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_
                              const uint32_t* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-#define PBFTV_WAVE(G, Q) launch_wave_w<G, Q>(hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes, st)
-  if (wg == 26 && wq == 22) PBFTV_WAVE(26, 22);
-  else if (wg == 26 && wq == 24) PBFTV_WAVE(26, 24);
-  else if (wg == 26 && wq == 20) PBFTV_WAVE(26, 20);
-  else if (wg == 26 && wq == 16) PBFTV_WAVE(26, 16);
-  else if (wg == 24 && wq == 22) PBFTV_WAVE(24, 22);
-  else if (wg == 24 && wq == 24) PBFTV_WAVE(24, 24);
-  else if (wg == 24 && wq == 20) PBFTV_WAVE(24, 20);
-  else if (wg == 20 && wq == 20) PBFTV_WAVE(20, 20);
-  else if (wg == 24 && wq == 16) PBFTV_WAVE(24, 16);
-  else if (wg == 16 && wq == 16) PBFTV_WAVE(16, 16);
-  else if (wg == 16 && wq == 12) PBFTV_WAVE(16, 12);
-  else if (wg == 16 && wq == 8) PBFTV_WAVE(16, 8);
-  else if (wg == 8 && wq == 8) PBFTV_WAVE(8, 8);
-  else return hipErrorInvalidValue;
+#define PBFTV_WAVE(G, Q)                                                                                    \
+  if (wg == G && wq == Q) {                                                                                   \
+    launch_wave_w<G, Q>(hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes, st);        \
+    return hipGetLastError();                                                                                 \
+  }
+  PBFTV_COMBOS(PBFTV_WAVE)
 #undef PBFTV_WAVE
-  return hipGetLastError();
+  return hipErrorInvalidValue;
 }
 
 uint64_t wave_path_max() {
@@ -930,56 +1055,51 @@ size_t scalar_prefix_bytes(uint64_t n) {
 template <int K>
 static void launch_scalars_k(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                              const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, uint32_t* prefix,
-                             hipStream_t st) {
+                             const uint32_t* perm, hipStream_t st) {
   const uint64_t lanes = (n + K - 1) / K;
   const uint64_t blocks = (lanes + 255) / 256;
   hipLaunchKernelGGL(k_ecdsa_scalars<K>, dim3((uint32_t)blocks), dim3(256), 0, st, hashes, sigs, key_idx, n,
-                     key_valid, nkeys, reinterpret_cast<uint4*>(scal), flag, prefix);
+                     key_valid, nkeys, reinterpret_cast<uint4*>(scal), flag, prefix, perm);
 }
 
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                                 const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, void* prefix,
-                                hipStream_t st) {
+                                const uint32_t* perm, hipStream_t st) {
   if (n == 0) return hipSuccess;
   uint32_t* pf = reinterpret_cast<uint32_t*>(prefix);
   switch (scalar_batch(n)) {
-    case 1: launch_scalars_k<1>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
-    case 2: launch_scalars_k<2>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
-    case 4: launch_scalars_k<4>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
-    case 8: launch_scalars_k<8>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
-    default: launch_scalars_k<16>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, st); break;
+    case 1: launch_scalars_k<1>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
+    case 2: launch_scalars_k<2>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
+    case 4: launch_scalars_k<4>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
+    case 8: launch_scalars_k<8>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
+    default: launch_scalars_k<16>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
   }
   return hipGetLastError();
 }
 
 template <int WG, int WQ>
 static void launch_comb_w(const void* scal, const uint8_t* flag, const uint8_t* sigs, const uint32_t* key_idx,
-                          uint64_t n, const uint32_t* gtab, const uint32_t* qtabs, uint8_t* bitmap, hipStream_t st) {
+                          uint64_t n, const uint32_t* gtab, const uint32_t* qtabs, uint8_t* bitmap,
+                          const uint32_t* perm, uint8_t* okb, hipStream_t st) {
   const uint64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL((k_ecdsa_comb<WG, WQ>), dim3((uint32_t)blocks), dim3(256), 0, st,
                      reinterpret_cast<const uint4*>(scal), flag, sigs, key_idx, n,
-                     reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4*>(qtabs), bitmap);
+                     reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4*>(qtabs), bitmap, perm, okb);
 }
 
 hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* flag, const uint8_t* sigs,
                              const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
-                             uint8_t* bitmap, hipStream_t st) {
+                             uint8_t* bitmap, const uint32_t* perm, uint8_t* okb, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (wg == 26 && wq == 22) launch_comb_w<26, 22>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 26 && wq == 24) launch_comb_w<26, 24>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 26 && wq == 20) launch_comb_w<26, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 26 && wq == 16) launch_comb_w<26, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 24 && wq == 22) launch_comb_w<24, 22>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 24 && wq == 24) launch_comb_w<24, 24>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 24 && wq == 20) launch_comb_w<24, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 20 && wq == 20) launch_comb_w<20, 20>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 24 && wq == 16) launch_comb_w<24, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 16 && wq == 16) launch_comb_w<16, 16>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 16 && wq == 12) launch_comb_w<16, 12>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 16 && wq == 8) launch_comb_w<16, 8>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else if (wg == 8 && wq == 8) launch_comb_w<8, 8>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, st);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (perm != nullptr && okb == nullptr) return hipErrorInvalidValue;
+#define PBFTV_COMB(G, Q)                                                                       \
+  if (wg == G && wq == Q) {                                                                    \
+    launch_comb_w<G, Q>(scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, perm, okb, st);     \
+    return hipGetLastError();                                                                  \
+  }
+  PBFTV_COMBOS(PBFTV_COMB)
+#undef PBFTV_COMB
+  return hipErrorInvalidValue;
 }
 
 size_t ecdsa_scratch_bytes(uint64_t n) { return (size_t)n * 64 + (size_t)n; }

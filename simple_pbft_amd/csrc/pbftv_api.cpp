@@ -105,6 +105,7 @@ struct Device {
   bool have_keys = false;
   // ecdsa scratch
   DevBuf hashes, sigs, key_idx, scal, flag, prefix, bitmap;
+  DevBuf ksort, okb;  // key order of the lane path (perm + counts) and its per-signature results
   HostBuf stage;  // zero-copy inputs/outputs of the small-batch path
   // sha scratch
   DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
@@ -377,6 +378,10 @@ int pbftv_reserve(pbftv_ctx* ctx, uint64_t n) {
     HIP_TRY(d.scal.ensure(n * 64));
     HIP_TRY(d.flag.ensure(n));
     HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
+    if (pbftv::key_sort_wanted(n, d.nkeys)) {
+      HIP_TRY(d.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
+      HIP_TRY(d.okb.ensure(n));
+    }
   }
   return PBFTV_OK;
 }
@@ -475,53 +480,55 @@ int pbftv_reset_kernel_times(pbftv_ctx* ctx) {
 }
 
 // ---------------------------------------------------------------- keys
-// Comb widths: G always 16-bit windows (34 MiB, shared); keys the widest of
-// 16 / 12 / 8 whose tables fit the budget (PBFTV_TABLE_BUDGET_MB, default
-// min(16 GiB, free HBM / 4)).  PBFTV_GBITS / PBFTV_QBITS override.
+// Comb geometry codes (p256_algo.h CombGeom): W-bit windows, or the mixed
+// 21 (5 x 22 + 7 x 21 bits) and 29 (5 x 29 + 4 x 28).  PBFTV_GBITS /
+// PBFTV_QBITS force one.
 static int env_bits(const char* name, int dflt) {
   const char* e = getenv(name);
   if (!e) return dflt;
   const int v = atoi(e);
-  return (v == 8 || v == 12 || v == 16 || v == 20 || v == 22 || v == 24 || v == 26) ? v : dflt;
+  return (v == 8 || v == 12 || v == 16 || v == 20 || v == 21 || v == 22 || v == 24 || v == 26 || v == 29) ? v : dflt;
 }
 
-// Comb widths (G, keys) with instantiated kernels; the widest that fit win
-// (fewer windows = fewer mixed additions per verify).
+// (G, keys) pairs with instantiated kernels
 static bool combo_ok(int wg, int wq) {
-  static const int kCombos[][2] = {{26, 24}, {26, 22}, {26, 20}, {26, 16}, {24, 24}, {24, 22}, {24, 20},
-                                   {20, 20}, {24, 16}, {16, 16}, {16, 12}, {16, 8},  {8, 8}};
-  for (auto& c : kCombos)
-    if (c[0] == wg && c[1] == wq) return true;
+#define PBFTV_PAIR(G, Q) \
+  if (wg == G && wq == Q) return true;
+  PBFTV_COMBOS(PBFTV_PAIR)
+#undef PBFTV_PAIR
   return false;
 }
 
-// HBM kept free for batch buffers and other users of the device.
-constexpr size_t kTableReserve = 64ull << 30;
+// HBM kept free for batch buffers, table-build scratch (~2 GB for 100 keys)
+// and other users of the device.
+constexpr size_t kTableReserve = 16ull << 30;
 
-// Table geometry: the pair (G, keys) with the fewest windows in total whose
-// tables fit the device's free HBM minus kTableReserve (an MI355X has 288 GB:
-// G at 26-bit windows = 21.5 GB; 4 keys at 24-bit = 23.6 GB; 100 keys at
-// 22-bit = 161 GB; 1000 keys at 16-bit = 35 GB).  Among equal totals the
-// narrower G wins (less HBM).  PBFTV_TABLE_BUDGET_MB caps the key tables;
-// PBFTV_GBITS / PBFTV_QBITS force a width.
+// Table geometry: the pair (G, keys) with the fewest windows in total (= mixed
+// additions per verify) whose tables fit the device's free HBM minus
+// kTableReserve.  An MI355X has 288 GB: G at 29 (mixed) = 120 GB, at 26 =
+// 21.5 GB; a key at 24 = 5.9 GB, at 21 (mixed) = 1.14 GB; so 4 keys run
+// 9 + 11 windows (144 GB), 100 keys 9 + 12 (234 GB), 1000 keys at 16-bit
+// 9 + 17.  Among equal totals the narrower G wins, and for each G the key
+// width with the fewest windows, then the least HBM (21 before 22: both 12
+// windows).  PBFTV_TABLE_BUDGET_MB caps the key tables.
 static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
   const uint64_t kk = k ? k : 1;
   const char* env_budget = getenv("PBFTV_TABLE_BUDGET_MB");
   const int force_g = env_bits("PBFTV_GBITS", 0), force_q = env_bits("PBFTV_QBITS", 0);
-  auto windows = [](int w) { return 256 / w + 1; };
   int best_g = 0, best_q = 0, best_win = 1 << 30;
-  for (int g : {16, 20, 24, 26}) {
+  for (int g : {16, 20, 24, 26, 29}) {
     if (force_g && g != force_g) continue;
     const size_t gb = pbftv::table_bytes(g);
     size_t budget = free_bytes > kTableReserve + gb ? free_bytes - kTableReserve - gb : 0;
     if (g > 16 && budget == 0 && !force_g) continue;  // wide G tables only with room to spare
-    budget = std::max(budget, free_bytes / 8);
+    if (g <= 26) budget = std::max(budget, free_bytes / 8);
     if (env_budget) budget = (size_t)atoll(env_budget) << 20;
-    for (int q : {24, 22, 20, 16, 12, 8}) {
+    for (int q : {24, 21, 22, 20, 16, 12, 8}) {
       if (force_q && q != force_q) continue;
+      if (q == 22 && !force_q) continue;  // same windows as 21, 40 % more HBM
       if (!combo_ok(g, q)) continue;
       if (!force_q && q > 8 && kk * pbftv::table_bytes(q) > budget) continue;
-      const int win = windows(g) + windows(q);
+      const int win = pbftv::table_windows(g) + pbftv::table_windows(q);
       if (win < best_win) {
         best_win = win;
         best_g = g;
@@ -532,8 +539,12 @@ static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
   }
   if (!best_g) {  // forced pair without an instantiated kernel: nearest G for the key width
     best_q = force_q ? force_q : 8;
-    best_g = best_q >= 20 ? 24 : (best_q == 8 && force_g == 8 ? 8 : 16);
-    if (!combo_ok(best_g, best_q)) best_g = 16;
+    best_g = 16;
+    for (int g : {force_g, 24, 26, 16, 29})
+      if (g && combo_ok(g, best_q)) {
+        best_g = g;
+        break;
+      }
   }
   *wg = best_g;
   *wq = best_q;
@@ -633,14 +644,23 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   HIP_TRY(d.scal.ensure(n * 64));
   HIP_TRY(d.flag.ensure(n));
   HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
+  const bool sorted = pbftv::key_sort_wanted(n, d.nkeys);
+  if (sorted) {  // comb lanes in key order: a wave's table lookups share keys (p256_kernels.hip k_key_*)
+    HIP_TRY(d.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
+    HIP_TRY(d.okb.ensure(n));
+    HIP_TRY(pbftv::launch_key_sort(d_key_idx, n, d.nkeys, d.ksort.p, st));
+  }
+  const uint32_t* perm = sorted ? d.ksort.as<uint32_t>() : nullptr;
   HIP_TRY(timed(d, PBFTV_K_ECDSA_SCALARS, st, [&] {
     return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, d.scal.p,
-                                       d.flag.as<uint8_t>(), d.prefix.p, st);
+                                       d.flag.as<uint8_t>(), d.prefix.p, perm, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
     return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.scal.p, d.flag.as<uint8_t>(), d_sigs, d_key_idx, n,
-                                    d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(), d_bitmap, st);
+                                    d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(), d_bitmap, perm,
+                                    sorted ? d.okb.as<uint8_t>() : nullptr, st);
   }));
+  if (sorted) HIP_TRY(pbftv::launch_pack_bits(d.okb.as<uint8_t>(), n, d_bitmap, st));
   return PBFTV_OK;
 }
 

@@ -145,6 +145,7 @@ int h_build_table_w(const uint8_t* pub_xy, int w, uint32_t* table) {
     case 8: return build_w<8>(pub_xy, table);
     case 10: return build_w<10>(pub_xy, table);
     case 12: return build_w<12>(pub_xy, table);
+    case 11: return build_w<11>(pub_xy, table);  // mixed: 15 x 12 + 7 x 11 bits
     default: return -1;
   }
 }
@@ -159,14 +160,15 @@ int h_verify_w(int w, const uint8_t* hash, const uint8_t* rs, const uint32_t* gt
   if (!ecdsa_scalars(e, r, s, u1, u2)) return 0;
   bool ok = false;
   auto run = [&](auto geom) {
-    constexpr int W = decltype(geom)::kW;
-    auto lg = [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + ((uint64_t)win * CombGeom<W>::kEnt + idx) * 16, 64); };
-    auto lq = [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + ((uint64_t)win * CombGeom<W>::kEnt + idx) * 16, 64); };
+    constexpr int W = decltype(geom)::kCode;
+    auto lg = [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + (CombGeom<W>::base(win) + idx) * 16, 64); };
+    auto lq = [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + (CombGeom<W>::base(win) + idx) * 16, 64); };
     ok = comb2_verify<W, W>(u1, u2, r, lg, lq);
   };
   if (w == 8) run(CombGeom<8>());
   else if (w == 10) run(CombGeom<10>());
   else if (w == 12) run(CombGeom<12>());
+  else if (w == 11) run(CombGeom<11>());
   else return -1;
   return ok ? 1 : 0;
 }

@@ -192,6 +192,30 @@ def test_pipeline_crafted_exceptional_sums(H):
         assert bool(got) == expect[i], i
 
 
+def test_pipeline_mixed_window_geometry(H, ecdsa_fixtures):
+    """A mixed comb geometry (p256_algo.h CombGeom code 11: 15 windows of 12
+    bits + 7 top windows of 11 bits = 257, the scheme of the device's 21 and 29
+    codes) -- recoding, per-window offsets and the half-size top windows --
+    on the golden vectors and the crafted doubling/cancellation sums."""
+    words = (15 * 2048 + 7 * 1024) * 16
+    g = (ctypes.c_uint32 * words)()
+    assert H.h_build_table_w(None, 11, g) == 1
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    tabs, valid = {}, {}
+    for k in sorted(set(int(x) for x in kidx if x < len(keys))):
+        t = (ctypes.c_uint32 * words)()
+        valid[k] = H.h_build_table_w(keys[k].tobytes(), 11, t)
+        tabs[k] = t
+    for i in range(len(kidx)):
+        k = int(kidx[i])
+        got = H.h_verify_w(11, hashes[i].tobytes(), sigs[i].tobytes(), g, tabs[k], valid[k]) if k in tabs else 0
+        assert got in (0, 1)
+        assert bool(got) == expect[i], ecdsa_fixtures["vectors"][i]["kind"]
+    key, hashes, sigs, kidx, expect = crafted_exceptional()
+    for i in range(len(kidx)):  # Q = G: the G table serves as the key table
+        assert bool(H.h_verify_w(11, hashes[i].tobytes(), sigs[i].tobytes(), g, g, 1)) == expect[i], i
+
+
 # ---- safegcd inversion mod n (simple_pbft_amd/csrc/safegcd.h) ----------------
 def _w8(v):
     return (ctypes.c_uint32 * 8)(*[(v >> 32 * i) & 0xFFFFFFFF for i in range(8)])

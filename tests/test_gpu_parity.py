@@ -7,7 +7,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import crafted_exceptional, fixture_arrays, oracle_sign_pool
+from conftest import fixture_arrays, oracle_sign_pool
 
 pytestmark = pytest.mark.gpu
 
@@ -189,29 +189,6 @@ def test_ecdsa_random_vs_oracle(ver, oracle_lib, path):
     assert want.sum() > n // 2
 
 
-@pytest.mark.parametrize("gq", [(26, 24), (26, 22), (26, 20), (26, 16), (24, 24), (24, 22), (24, 20), (20, 20), (24, 16),
-                                (16, 16), (16, 12), (16, 8), (8, 8)])
-def test_ecdsa_every_table_width(oracle_lib, ecdsa_fixtures, gq, path, monkeypatch):
-    """Golden vectors + random corruptions vs the oracle for every comb geometry."""
-    from simple_pbft_amd import Verifier
-    monkeypatch.setenv("PBFTV_GBITS", str(gq[0]))
-    monkeypatch.setenv("PBFTV_QBITS", str(gq[1]))
-    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
-    with Verifier() as v:
-        assert v.register_keys(keys).tolist() == [k["valid"] for k in ecdsa_fixtures["keys"]]
-        assert v.table_config()[:2] == gq
-        assert (v.verify_batch(hashes, sigs, kidx) == expect).all()
-        pk, h, sg, ki = oracle_sign_pool(oracle_lib, n_keys=5, per_key=50, seed=gq[0] * 100 + gq[1])
-        sg[::3, 7] ^= 0x20
-        v.register_keys(pk)
-        got = v.verify_batch(h, sg, ki)
-        n = len(ki)
-        bm = np.zeros((n + 7) // 8, np.uint8)
-        oracle_lib.oracle_ecdsa_p256_verify_batch(h.ctypes.data, sg.ctypes.data, ki.ctypes.data, n, pk.ctypes.data,
-                                                  len(pk), bm.ctypes.data, 8)
-        assert (got == np.unpackbits(bm, bitorder="little")[:n].astype(bool)).all()
-
-
 @pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
 def test_ecdsa_scalar_batch_sizes(ver, oracle_lib, ecdsa_fixtures, k, monkeypatch):
     """The batched-inversion scalar kernel for every K (signatures per lane),
@@ -239,6 +216,49 @@ def test_ecdsa_large_tiled_property(ver, oracle_lib):
     bad = rng.random(len(K)) < 0.01
     idx = np.nonzero(bad)[0]
     S[idx, 63] ^= 1
+    ver.register_keys(keys)
+    got = ver.verify_batch(H, S, K)
+    assert (got == ~bad).all()
+
+
+@pytest.mark.parametrize("sort", ["0", "1"])
+def test_ecdsa_key_order(ver, oracle_lib, sort, monkeypatch):
+    """The lane path with and without the key-order stage (k_key_* + k_pack_bits):
+    shuffled signatures of 24 keys, a ragged count, corruptions, out-of-range
+    key indices and an invalid registered key, against the oracle."""
+    monkeypatch.setenv("PBFTV_WAVE_MAX", "0")
+    monkeypatch.setenv("PBFTV_KEY_SORT", sort)
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=24, per_key=125, seed=77)
+    rng = np.random.default_rng(78)
+    o = rng.permutation(len(kidx))[:2999]
+    hashes, sigs, kidx = hashes[o].copy(), sigs[o].copy(), kidx[o].copy()
+    n = len(kidx)
+    sel = rng.random(n) < 0.2
+    sigs[sel, 40] ^= 0x08
+    kidx[rng.random(n) < 0.02] = 24 + rng.integers(0, 1000)   # no such key
+    keys = keys.copy()
+    keys[5, 63] ^= 1                                           # key 5 off the curve: its signatures fail
+    ver.register_keys(keys)
+    got = ver.verify_batch(hashes, sigs, kidx)
+    want = np.zeros((n + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n].astype(bool)
+    assert (got == want).all()
+    assert want.sum() > n // 2
+
+
+def test_ecdsa_key_order_large_property(ver, oracle_lib):
+    """The default large-batch path (key order on: > 8 keys, n >= 32768): 131,072
+    tiled signatures of 100 keys in random order, 1 % corrupted at known
+    positions -- the bitmap must be the complement of the corruption mask."""
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=100, per_key=8, seed=321)
+    reps = 131072 // len(kidx) + 1
+    rng = np.random.default_rng(9)
+    o = rng.permutation(reps * len(kidx))[:131072] % len(kidx)
+    H, S, K = hashes[o], sigs[o].copy(), kidx[o]
+    bad = rng.random(len(K)) < 0.01
+    S[np.nonzero(bad)[0], 31] ^= 2
     ver.register_keys(keys)
     got = ver.verify_batch(H, S, K)
     assert (got == ~bad).all()
@@ -302,17 +322,3 @@ def test_ecdsa_wave_path_edge_counts(ver, oracle_lib, monkeypatch):
     for n in (1, 2, 7, 8, 9, 15, 16, 17, 67, 2047, 2048, 2049, 2400):
         got = ver.verify_batch(hashes[:n], sigs[:n], kidx[:n])
         assert (got == want[:n]).all(), n
-
-
-@pytest.mark.parametrize("gq", [(26, 24), (26, 22), (24, 24), (24, 22), (24, 20), (20, 20), (24, 16), (16, 16), (16, 8),
-                                (8, 8)])
-def test_ecdsa_crafted_exceptional_sums(gq, path, monkeypatch):
-    from simple_pbft_amd import Verifier
-    monkeypatch.setenv("PBFTV_GBITS", str(gq[0]))
-    monkeypatch.setenv("PBFTV_QBITS", str(gq[1]))
-    key, H, S, K, E = crafted_exceptional()
-    assert E.sum() >= 10  # the crafted ones verify, the r-flipped ones do not
-    with Verifier() as v:
-        v.register_keys(key)
-        assert v.table_config()[:2] == gq
-        assert (v.verify_batch(H, S, K) == E).all()

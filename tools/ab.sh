@@ -7,13 +7,13 @@ R=$1; shift
 mkdir -p gpurun_out/ab
 for r in $(seq 1 "$R"); do
   for v in base "$@"; do
-    # v = a library exp/libpbftv_<v>.so, or env:NAME=VALUE (same library, one variable set)
+    # v = a library exp/libpbftv_<v>.so, or env:NAME=VALUE[,NAME=VALUE...] (same library, variables set)
     L=""; E=""
     case "$v" in
       base) ;;
-      env:*) E=${v#env:} ;;
+      env:*) E=${v#env:}; E=${E//,/ } ;;
       *) L=$PWD/exp/libpbftv_$v.so ;;
     esac
-    env PBFTV_LIB=$L $E timeout -k 10 120 python bench.py --no-extras --steps 20 > "gpurun_out/ab/${v//[:=]/_}_$r.json" 2>&1
+    env PBFTV_LIB=$L $E timeout -k 10 120 python bench.py --no-extras --steps 20 > "gpurun_out/ab/${v//[:=,]/_}_$r.json" 2>&1
   done
 done

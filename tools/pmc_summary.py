@@ -7,6 +7,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -20,9 +21,13 @@ def short(name: str) -> str:
 
 def main(d: str):
     vals = defaultdict(lambda: defaultdict(list))
+    geom = {}
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             vals[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            g = re.search(r"k_ecdsa_comb<(\d+), (\d+)>", row["Kernel_Name"])
+            if g:
+                geom[(int(g.group(1)), int(g.group(2)))] = 1
     out = {}
     for k, cs in vals.items():
         m = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -36,7 +41,18 @@ def main(d: str):
         if "FETCH_SIZE" in m or "WRITE_SIZE" in m:
             m["hbm_bytes_per_launch"] = 2 * 1024 * m.get("FETCH_SIZE", 0) + 1024 * m.get("WRITE_SIZE", 0)
         out[k] = m
-    json.dump(out, sys.stdout, indent=1)
+    res = {"source": "rocprofv3 --pmc, separate passes (tools/pmc_passes.sh) over bench.py --steps 2 --warmup 1 "
+                     "--no-extras; means over dispatches; FETCH_SIZE/WRITE_SIZE in KiB, FETCH doubled (gfx950)",
+           "counters": out}
+    for k, m in out.items():
+        if k in ("ecdsa_comb", "ecdsa_scalars") and "hbm_bytes_per_launch" in m:
+            e = {"hbm_bytes_per_launch": m["hbm_bytes_per_launch"]}
+            if "SQ_INSTS_VALU" in m and m.get("SQ_WAVES"):
+                e["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / m["SQ_WAVES"]
+            if k == "ecdsa_comb" and len(geom) == 1:
+                e["geometry"] = list(next(iter(geom)))  # bench.py uses the traffic only for this geometry
+            res[k] = e
+    json.dump(res, sys.stdout, indent=1)
     print()
 
 
