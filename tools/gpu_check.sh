@@ -11,4 +11,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o run \
-  -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-extras > "$ROOT/$OUT/prof_bench.json" 2> "$ROOT/$OUT/prof.log"
+  -- python3 "$ROOT/bench.py" --no-extras > "$ROOT/$OUT/prof_bench.json" 2> "$ROOT/$OUT/prof.log"
