@@ -126,6 +126,13 @@ uint64_t pbftv_gojson_request(int64_t timestamp, const char* client_id, uint64_t
                               uint64_t operation_len, int64_t sequence_id, uint8_t* out, uint64_t cap);
 uint64_t pbftv_gojson_vote(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
                            const char* node_id, uint64_t node_id_len, int64_t msg_type, uint8_t* out, uint64_t cap);
+/* Signed VoteMsg on the wire (build-added; no reference
+ * counterpart): the VoteMsg fields of pbft_msg_types.go:25-31 followed by
+ * Signature []byte `json:"signature"` -- base64.StdEncoding, or null when
+ * sig_nil != 0 (Go's nil slice).  The signing preimage is pbftv_gojson_vote. */
+uint64_t pbftv_gojson_vote_signed(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                                  const char* node_id, uint64_t node_id_len, int64_t msg_type, const uint8_t* sig,
+                                  uint64_t sig_len, int sig_nil, uint8_t* out, uint64_t cap);
 uint64_t pbftv_gojson_reply(int64_t view_id, int64_t timestamp, const char* client_id, uint64_t client_id_len,
                             const char* node_id, uint64_t node_id_len, const char* result, uint64_t result_len,
                             uint8_t* out, uint64_t cap);
@@ -133,6 +140,16 @@ uint64_t pbftv_gojson_preprepare(int64_t view_id, int64_t sequence_id, const cha
                                  int has_request, int64_t req_timestamp, const char* req_client_id,
                                  uint64_t req_client_id_len, const char* req_operation, uint64_t req_operation_len,
                                  int64_t req_sequence_id, uint8_t* out, uint64_t cap);
+
+/* ---- DER signatures (go1.19 crypto/ecdsa.VerifyASN1's cryptobyte parse) ---
+ * SEQUENCE { INTEGER r, INTEGER s } with Go's DER strictness -> r||s (64 B
+ * big-endian, the sig_rs layout of pbftv_ecdsa_p256_verify_batch).  Returns 1
+ * when parsed with 0 <= r, s < 2^256, 0 when Go would reject it at the parse
+ * or range check (out_rs zeroed, so the verify yields a 0 bit), PBFTV_EINVAL
+ * on null pointers.  The batch form returns the number parsed (or < 0). */
+int pbftv_ecdsa_der_to_rs(const uint8_t* der, uint64_t der_len, uint8_t* out_rs);
+int64_t pbftv_ecdsa_der_to_rs_batch(const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                                    uint64_t n, uint8_t* out_rs);
 
 /* digest(*RequestMsg) for n requests (pbft_impl.go:235-243, called from
  * StartConsensus :73 and verifyMsg :190): the struct fields are shipped

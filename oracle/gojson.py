@@ -89,6 +89,15 @@ def vote(view_id: int, sequence_id: int, digest: bytes, node_id: bytes, msg_type
             b',"nodeID":' + string(node_id) + b',"msgType":' + _int(msg_type) + b"}")
 
 
+def vote_signed(view_id: int, sequence_id: int, digest: bytes, node_id: bytes, msg_type: int,
+                signature: bytes | None) -> bytes:
+    """Signed VoteMsg wire JSON (build-added field after the embedded MsgType):
+    Go encodes a []byte as a base64.StdEncoding string and a nil slice as null."""
+    import base64
+    sig = b"null" if signature is None else b'"' + base64.b64encode(signature) + b'"'
+    return vote(view_id, sequence_id, digest, node_id, msg_type)[:-1] + b',"signature":' + sig + b"}"
+
+
 def reply(view_id: int, timestamp: int, client_id: bytes, node_id: bytes, result: bytes) -> bytes:
     """ReplyMsg, pbft_msg_types.go:10-16."""
     return (b'{"viewID":' + _int(view_id) + b',"timestamp":' + _int(timestamp) + b',"clientID":' + string(client_id) +

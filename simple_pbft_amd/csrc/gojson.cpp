@@ -42,6 +42,13 @@ void append_vote(std::vector<uint8_t>& o, int64_t view, int64_t seq, const uint8
   vote(k, view, seq, dg, dgn, nid, nidn, mt);
 }
 
+void append_vote_signed(std::vector<uint8_t>& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t dgn,
+                        const uint8_t* nid, uint64_t nidn, int64_t mt, const uint8_t* sig, uint64_t sign,
+                        bool sig_nil) {
+  VecSink k{o};
+  vote_signed(k, view, seq, dg, dgn, nid, nidn, mt, sig, sign, sig_nil);
+}
+
 void append_reply(std::vector<uint8_t>& o, int64_t view, int64_t ts, const uint8_t* cid, uint64_t cidn,
                   const uint8_t* nid, uint64_t nidn, const uint8_t* res, uint64_t resn) {
   VecSink k{o};

@@ -21,6 +21,10 @@ void append_request(std::vector<uint8_t>& out, int64_t timestamp, const uint8_t*
 // VoteMsg (pbft_msg_types.go:25-31)
 void append_vote(std::vector<uint8_t>& out, int64_t view_id, int64_t sequence_id, const uint8_t* digest,
                  uint64_t digest_len, const uint8_t* node_id, uint64_t node_id_len, int64_t msg_type);
+// signed VoteMsg wire encoding: VoteMsg + "signature":<base64 | null>
+void append_vote_signed(std::vector<uint8_t>& out, int64_t view_id, int64_t sequence_id, const uint8_t* digest,
+                        uint64_t digest_len, const uint8_t* node_id, uint64_t node_id_len, int64_t msg_type,
+                        const uint8_t* sig, uint64_t sig_len, bool sig_nil);
 // ReplyMsg (pbft_msg_types.go:10-16)
 void append_reply(std::vector<uint8_t>& out, int64_t view_id, int64_t timestamp, const uint8_t* client_id,
                   uint64_t client_id_len, const uint8_t* node_id, uint64_t node_id_len, const uint8_t* result,

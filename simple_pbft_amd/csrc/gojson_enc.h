@@ -150,6 +150,55 @@ PBFTV_GJ void vote(S& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t 
 }
 PBFTV_GJ uint64_t vote_bound(uint64_t dgn, uint64_t nidn) { return 120 + 6 * (dgn + nidn); }
 
+// []byte field (encoding/json encodeByteSlice, go1.19): nil -> null, otherwise
+// a quoted base64.StdEncoding string (padded, no line breaks)
+template <class S>
+PBFTV_GJ void put_bytes(S& o, const uint8_t* b, uint64_t n, bool is_nil) {
+  if (is_nil) {
+    lit(o, "null");
+    return;
+  }
+  const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  o.put('"');
+  uint64_t i = 0;
+  for (; i + 3 <= n; i += 3) {
+    const uint32_t v = ((uint32_t)b[i] << 16) | ((uint32_t)b[i + 1] << 8) | b[i + 2];
+    uint8_t* w = o.grow(4);
+    w[0] = (uint8_t)A[v >> 18]; w[1] = (uint8_t)A[(v >> 12) & 63]; w[2] = (uint8_t)A[(v >> 6) & 63]; w[3] = (uint8_t)A[v & 63];
+  }
+  if (n - i == 1) {
+    const uint32_t v = (uint32_t)b[i] << 16;
+    uint8_t* w = o.grow(4);
+    w[0] = (uint8_t)A[v >> 18]; w[1] = (uint8_t)A[(v >> 12) & 63]; w[2] = '='; w[3] = '=';
+  } else if (n - i == 2) {
+    const uint32_t v = ((uint32_t)b[i] << 16) | ((uint32_t)b[i + 1] << 8);
+    uint8_t* w = o.grow(4);
+    w[0] = (uint8_t)A[v >> 18]; w[1] = (uint8_t)A[(v >> 12) & 63]; w[2] = (uint8_t)A[(v >> 6) & 63]; w[3] = '=';
+  }
+  o.put('"');
+}
+
+// Signed VoteMsg on the wire (build-added): the fields of
+// pbft_msg_types.go:25-31 followed by  Signature []byte `json:"signature"`.
+// The signing preimage is vote() above (the struct without the signature).
+template <class S>
+PBFTV_GJ void vote_signed(S& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t dgn, const uint8_t* nid,
+                          uint64_t nidn, int64_t mt, const uint8_t* sig, uint64_t sign, bool sig_nil) {
+  lit(o, "{\"viewID\":");
+  put_int(o, view);
+  lit(o, ",\"sequenceID\":");
+  put_int(o, seq);
+  lit(o, ",\"digest\":");
+  put_string(o, dg, dgn);
+  lit(o, ",\"nodeID\":");
+  put_string(o, nid, nidn);
+  lit(o, ",\"msgType\":");
+  put_int(o, mt);
+  lit(o, ",\"signature\":");
+  put_bytes(o, sig, sign, sig_nil);
+  o.put('}');
+}
+
 // ReplyMsg (pbft_msg_types.go:10-16)
 template <class S>
 PBFTV_GJ void reply(S& o, int64_t view, int64_t ts, const uint8_t* cid, uint64_t cidn, const uint8_t* nid,

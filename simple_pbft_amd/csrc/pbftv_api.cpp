@@ -1113,6 +1113,17 @@ uint64_t pbftv_gojson_vote(int64_t view_id, int64_t sequence_id, const char* dig
   return b.size();
 }
 
+uint64_t pbftv_gojson_vote_signed(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                                  const char* node_id, uint64_t node_id_len, int64_t msg_type, const uint8_t* sig,
+                                  uint64_t sig_len, int sig_nil, uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_vote_signed(b, view_id, sequence_id, reinterpret_cast<const uint8_t*>(digest), digest_len,
+                                    reinterpret_cast<const uint8_t*>(node_id), node_id_len, msg_type, sig, sig_len,
+                                    sig_nil != 0);
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
 uint64_t pbftv_gojson_reply(int64_t view_id, int64_t timestamp, const char* client_id, uint64_t client_id_len,
                             const char* node_id, uint64_t node_id_len, const char* result, uint64_t result_len,
                             uint8_t* out, uint64_t cap) {

@@ -78,6 +78,12 @@ def lib() -> ctypes.CDLL:
         "pbftv_gojson_vote": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64,
                                                 ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int64, _vp,
                                                 ctypes.c_uint64]),
+        "pbftv_gojson_vote_signed": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p,
+                                                       ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                                                       ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
+                                                       _vp, ctypes.c_uint64]),
+        "pbftv_ecdsa_der_to_rs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _vp]),
+        "pbftv_ecdsa_der_to_rs_batch": (ctypes.c_int64, [_vp, _vp, _vp, ctypes.c_uint64, _vp]),
         "pbftv_gojson_reply": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64,
                                                  ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                                  _vp, ctypes.c_uint64]),
@@ -154,6 +160,44 @@ def gojson_vote(view: int, seq: int, digest: bytes, node_id: bytes, msg_type: in
     buf = np.zeros(max(n, 1), np.uint8)
     L.pbftv_gojson_vote(view, seq, digest, len(digest), node_id, len(node_id), msg_type, buf.ctypes.data, n)
     return buf[:n].tobytes()
+
+
+def gojson_vote_signed(view: int, seq: int, digest: bytes, node_id: bytes, msg_type: int,
+                       signature: bytes | None) -> bytes:
+    """Signed VoteMsg wire JSON: VoteMsg + "signature" as base64, None -> null."""
+    L = lib()
+    sig = signature if signature is not None else b""
+    args = (view, seq, digest, len(digest), node_id, len(node_id), msg_type, sig, len(sig),
+            1 if signature is None else 0)
+    n = L.pbftv_gojson_vote_signed(*args, None, 0)
+    buf = np.zeros(max(n, 1), np.uint8)
+    L.pbftv_gojson_vote_signed(*args, buf.ctypes.data, n)
+    return buf[:n].tobytes()
+
+
+def der_to_rs(der: bytes) -> bytes | None:
+    """go1.19 ecdsa.VerifyASN1's DER parse: r||s (64 B BE), or None where Go rejects."""
+    out = np.zeros(64, np.uint8)
+    r = lib().pbftv_ecdsa_der_to_rs(der, len(der), out.ctypes.data)
+    if r < 0:
+        raise ValueError(f"pbftv_ecdsa_der_to_rs: {r}")
+    return out.tobytes() if r == 1 else None
+
+
+def der_to_rs_batch(ders: list[bytes]) -> tuple[np.ndarray, int]:
+    """Batch form: (n x 64 uint8 r||s, rejected rows zeroed; number parsed)."""
+    n = len(ders)
+    lens = np.array([len(d) for d in ders], np.uint32)
+    offs = np.zeros(n, np.uint64)
+    if n > 1:
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    data = np.frombuffer(b"".join(ders) + b"\0", np.uint8)
+    out = np.zeros((max(n, 1), 64), np.uint8)
+    got = lib().pbftv_ecdsa_der_to_rs_batch(data.ctypes.data, offs.ctypes.data, lens.ctypes.data, n,
+                                            out.ctypes.data)
+    if got < 0:
+        raise ValueError(f"pbftv_ecdsa_der_to_rs_batch: {got}")
+    return out[:n], int(got)
 
 
 def gojson_reply(view: int, ts: int, client_id: bytes, node_id: bytes, result: bytes) -> bytes:
