@@ -348,12 +348,6 @@ def main():
     ver = Verifier(device_mask=1 if share else 1 << local)
     n = args.n
     pub, H, S, K, ok = synth.config4(n, n_keys=args.keys, seed=0x50424654 + rank)
-    sk = int(os.environ.get("PBFTV_EXP_SORT_KEYS", "0"))
-    if sk:  # experiment only: batch pre-sorted by key (1: whole batch, c: within chunks of c) -- not a bench line
-        c = n if sk == 1 else sk
-        o = (np.arange(n) // c).astype(np.int64) * (1 << 32) + K
-        o = np.argsort(o, kind="stable")
-        H, S, K, ok = H[o], S[o], K[o], ok[o]
     valid = ver.register_keys(pub)
     assert valid.all()
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)

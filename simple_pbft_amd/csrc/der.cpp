@@ -9,8 +9,10 @@
 // readASN1: single-byte tags only (low 5 bits != 0x1f); short-form length, or
 // long form with 1..4 length bytes, value >= 128 and no leading zero byte.
 // checkASN1Integer: non-empty, minimal two's complement (no redundant 0x00 /
-// 0xff lead byte).  A negative or zero integer or one >= 2^256 can never pass
+// 0xff lead byte).  A negative integer or one >= 2^256 can never pass
 // Verify's 1 <= r, s < n test, so it is rejected here (rs zeroed -> 0 bit).
+// A zero integer parses (as in Go: ReadASN1Integer accepts 0) and is rejected
+// by the verify kernels' range check, like any r or s >= n.
 #include <cstdint>
 #include <cstring>
 
@@ -86,6 +88,9 @@ int64_t pbftv_ecdsa_der_to_rs_batch(const uint8_t* data, const uint64_t* offsets
                                     uint64_t n, uint8_t* out_rs) {
   if (n == 0) return 0;
   if (offsets == nullptr || lengths == nullptr || out_rs == nullptr) return -1;
+  if (data == nullptr)
+    for (uint64_t i = 0; i < n; ++i)
+      if (lengths[i] != 0) return -1;  // PBFTV_EINVAL: encodings promised but no bytes
   int64_t parsed = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const int r = pbftv_ecdsa_der_to_rs(data ? data + offsets[i] : nullptr, data ? lengths[i] : 0, out_rs + 64 * i);

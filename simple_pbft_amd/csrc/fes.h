@@ -1,0 +1,211 @@
+// fes.h -- signed-limb P-256 field arithmetic for the comb's hot loop (gfx950).
+//
+// Same numbers as fe29.h (9 limbs of 29 bits, value = sum v[i] 2^(29 i),
+// Montgomery R = 2^261), but limbs are SIGNED 32-bit and products accumulate
+// through v_mad_i64_i32 into signed 64-bit columns.  What that buys
+// (DESIGN.md "Signed limbs"):
+//   * a subtraction is 9 v_sub_u32 -- no carry chain, no fold of bits >= 2^256
+//     (fe_sub: ~40 VALU instructions);
+//   * the Montgomery digit of column i is its low 32 bits as they stand
+//     (m = lo32(t_i) == t_i mod 2^29) and the column's carry is
+//     hi32(t_i) * 8, ONE v_mad_i64_i32 -- no mask, no 64-bit shift + add
+//     (fe29.h: and + v_lshrrev_b64 + v_lshl_add_u64).  The top digit is kept at
+//     29 bits so the output stays below T / 2^261 + 1.0001 p;
+//   * the -m 2^224 term of m p is added as (~m) 2^21 into column i+7, whose
+//     constant surplus (2^32 - 1) 2^21 is pre-subtracted from the column
+//     (exact integer arithmetic: no bias mod p).
+//
+// Types (checked by tests/test_algo_cpu.py, CPU harness):
+//   S (product output, fs_norm output): limbs 0..7 in [0, 2^29), limb 8 signed,
+//       |value| < 2^257.5;
+//   D (difference of two S): |limbs| < 2^29, |value| < 2^258.5;
+//   canonical table coordinates and their negatives are D-type.
+// Products need max|a_i| * max|b_j| <= 2^59 (columns stay below 2^62.3 in
+// magnitude): S x S, S x D, D x D, and fs_mul2_add of two such pairs.
+//
+// Compiled by hipcc for the device and by g++ for the CPU test harness only.
+#pragma once
+#include "fe29.h"
+
+namespace pbftv {
+
+// a * b with both limbs taken as signed 32-bit (v_mad_i64_i32 on the device)
+PBFTV_HD uint64_t smul(uint32_t a, uint32_t b) { return (uint64_t)((int64_t)(int32_t)a * (int64_t)(int32_t)b); }
+
+// surplus of the (~m) 2^21 terms: (2^32 - 1) 2^21 per 32-bit digit (columns
+// 7..14), (2^29 - 1) 2^21 for the 29-bit top digit (column 15)
+constexpr uint64_t kFsBias32 = (uint64_t)(-(int64_t)(0xFFFFFFFFull << 21));
+constexpr uint64_t kFsBias29 = (uint64_t)(-(int64_t)((uint64_t)kMask29 << 21));
+
+// The bias as a value the compiler cannot fold: on the device an SGPR pair,
+// so it becomes the addend of the column's first v_mad (no separate 64-bit add).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint64_t opaque_u64(uint64_t c) {
+  uint64_t r;
+  asm("s_mov_b64 %0, %1" : "=s"(r) : "s"(c));
+  return r;
+}
+#else
+static inline uint64_t opaque_u64(uint64_t c) { return c; }
+#endif
+
+PBFTV_HD void fs_cols_init(uint64_t t[17]) {
+  const uint64_t b32 = opaque_u64(kFsBias32), b29 = opaque_u64(kFsBias29);
+  PBFTV_UNROLL for (int k = 0; k < 17; ++k) t[k] = 0;
+  PBFTV_UNROLL for (int k = 7; k < 15; ++k) t[k] = b32;
+  t[15] = b29;
+}
+
+// Montgomery digit step of column i < 8 (32-bit digit, carry by one signed MAD)
+PBFTV_HD void fs_digit(uint64_t t[17], int i, uint32_t c8, uint32_t c9, uint32_t c18, uint32_t c21, uint32_t c24) {
+  const uint32_t m = (uint32_t)t[i];
+  const uint32_t h = (uint32_t)(t[i] >> 32);
+  t[i + 1] += smul(h, c8);
+  t[i + 3] += (uint64_t)m * c9;
+  t[i + 6] += (uint64_t)m * c18;
+  t[i + 7] += (uint64_t)(~m) * c21;
+  t[i + 8] += (uint64_t)m * c24;
+}
+
+// top digit (column 8): 29 bits, arithmetic carry
+PBFTV_HD void fs_digit_top(uint64_t t[17], uint32_t c9, uint32_t c18, uint32_t c21, uint32_t c24) {
+  const uint32_t m = (uint32_t)t[8] & kMask29;
+  t[9] += (uint64_t)((int64_t)t[8] >> 29);
+  t[11] += (uint64_t)m * c9;
+  t[14] += (uint64_t)m * c18;
+  t[15] += (uint64_t)(m ^ kMask29) * c21;
+  t[16] += (uint64_t)m * c24;
+}
+
+// columns 9..16 -> S-type limbs (signed carries)
+PBFTV_HD void fs_out(fe& r, uint64_t t[17]) {
+  PBFTV_UNROLL for (int j = 9; j < 16; ++j) {
+    r.v[j - 9] = (uint32_t)t[j] & kMask29;
+    t[j + 1] += (uint64_t)((int64_t)t[j] >> 29);
+  }
+  r.v[7] = (uint32_t)t[16] & kMask29;
+  r.v[8] = (uint32_t)((int64_t)t[16] >> 29);
+}
+
+#define PBFTV_FS_CONSTS                                                                                   \
+  const uint32_t c8 = opaque_u32(8u), c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18),               \
+                 c21 = opaque_u32(1u << 21), c24 = opaque_u32(1u << 24)
+
+// r = a b 2^-261 (mod p), S-type.  Digit step i right after product row i
+// (column i is final then), as in fe_mul.
+PBFTV_HD void fs_mul(fe& r, const fe& a, const fe& b) {
+  PBFTV_FS_CONSTS;
+  uint64_t t[17];
+  fs_cols_init(t);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += smul(a.v[i], b.v[j]);
+    if (i < 8) fs_digit(t, i, c8, c9, c18, c21, c24);
+    else fs_digit_top(t, c9, c18, c21, c24);
+  }
+  fs_out(r, t);
+}
+
+// r = (a b + c d) 2^-261 (mod p): one reduction for two products
+PBFTV_HD void fs_mul2_add(fe& r, const fe& a, const fe& b, const fe& c, const fe& d) {
+  PBFTV_FS_CONSTS;
+  uint64_t t[17];
+  fs_cols_init(t);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += smul(a.v[i], b.v[j]);
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += smul(c.v[i], d.v[j]);
+    if (i < 8) fs_digit(t, i, c8, c9, c18, c21, c24);
+    else fs_digit_top(t, c9, c18, c21, c24);
+  }
+  fs_out(r, t);
+}
+
+// r = a^2 2^-261 (mod p): 45 products, cross terms by the doubled limb
+// (|2 a_j| < 2^30: cross products < 2^59)
+PBFTV_HD void fs_sqr(fe& r, const fe& a) {
+  PBFTV_FS_CONSTS;
+  uint64_t t[17];
+  uint32_t a2[9];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) a2[i] = a.v[i] << 1;
+  fs_cols_init(t);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    t[2 * i] += smul(a.v[i], a.v[i]);
+    PBFTV_UNROLL for (int j = i + 1; j < 9; ++j) t[i + j] += smul(a.v[i], a2[j]);
+  }
+  PBFTV_UNROLL for (int i = 0; i < 8; ++i) fs_digit(t, i, c8, c9, c18, c21, c24);
+  fs_digit_top(t, c9, c18, c21, c24);
+  fs_out(r, t);
+}
+
+// r = a - b limb-wise (D-type for S-type inputs)
+PBFTV_HD void fs_sub(fe& r, const fe& a, const fe& b) {
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] - b.v[i];
+}
+
+PBFTV_HD void fs_neg(fe& r, const fe& a) {
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = 0u - a.v[i];
+}
+
+// r = neg ? -a : a  (mask select: (a ^ m) - m)
+PBFTV_HD void fs_cneg(fe& r, const fe& a, bool neg) {
+  const uint32_t m = 0u - (uint32_t)neg;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = (a.v[i] ^ m) - m;
+}
+
+// signed limbs (|l_i| < 2^31 - 2^3) -> S-type: one signed carry pass, no fold
+PBFTV_HD void fs_norm(fe& r, const fe& a) {
+  int32_t d[9];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) d[i] = (int32_t)a.v[i];
+  PBFTV_UNROLL for (int i = 0; i < 8; ++i) {
+    d[i + 1] += d[i] >> 29;
+    d[i] &= (int32_t)kMask29;
+  }
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = (uint32_t)d[i];
+}
+
+// canonical [0, p) of an S- or D-type value (via fe29.h's fold + conditional subtract)
+PBFTV_HD void fs_canon(fe& r, const fe& a) {
+  int32_t d[9];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) d[i] = (int32_t)a.v[i];
+  fe n;
+  fe_fold_carry(n, d);
+  fe_canon(r, n);
+}
+
+PBFTV_HD bool fs_is_zero(const fe& a) {
+  fe c;
+  fs_canon(c, a);
+  uint32_t o = 0;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) o |= c.v[i];
+  return o == 0;
+}
+
+// ---- XYZZ mixed addition on signed limbs (madd-2008-s, 8M + 2S) -------------
+// acc: X, Y, ZZ, ZZZ S-type; (x2, y2) D-type (a canonical table point, y2
+// possibly negated).  Unchecked, as xyzz_madd: a doubling or cancellation
+// leaves ZZ = ZZZ = 0, which later additions preserve.
+struct xyzz_s {
+  fe x, y, zz, zzz;
+};
+
+PBFTV_HD void xyzz_madd_s(xyzz_s& acc, const fe& x2, const fe& y2) {
+  fe u2, s2, p, r, pp, ppp, q, r2, t, ny;
+  fs_mul(u2, x2, acc.zz);
+  fs_mul(s2, y2, acc.zzz);
+  fs_sub(p, u2, acc.x);                // P = U2 - X1            D
+  fs_sub(r, s2, acc.y);                // R = S2 - Y1            D
+  fs_sqr(pp, p);
+  fs_mul(ppp, p, pp);
+  fs_mul(q, acc.x, pp);
+  fs_sqr(r2, r);
+  fe x3;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) x3.v[i] = r2.v[i] - ppp.v[i] - (q.v[i] << 1);
+  fs_norm(x3, x3);                     // X3 = R^2 - PPP - 2Q    S
+  fs_sub(t, q, x3);                    // Q - X3                 D
+  fs_neg(ny, acc.y);                   // -Y1                    D
+  fs_mul2_add(acc.y, r, t, ny, ppp);   // Y3 = R (Q - X3) - Y1 PPP, one reduction
+  fs_mul(acc.zz, acc.zz, pp);          // ZZ3 = ZZ1 PP
+  fs_mul(acc.zzz, acc.zzz, ppp);       // ZZZ3 = ZZZ1 PPP
+  acc.x = x3;
+}
+
+}  // namespace pbftv

@@ -13,9 +13,12 @@ namespace pbftv {
 size_t table_bytes(int w);
 int table_windows(int w);  // windows = table entries added per scalar
 // (G, key) geometry pairs with instantiated verify kernels
-#define PBFTV_COMBOS(X)                                                                                       \
-  X(29, 24) X(29, 22) X(29, 21) X(29, 20) X(29, 16) X(26, 24) X(26, 22) X(26, 21) X(26, 20) X(26, 16)          \
-  X(24, 24) X(24, 22) X(24, 20) X(20, 20) X(24, 16) X(16, 16) X(16, 12) X(16, 8) X(8, 8)
+// (split by G width into the instantiation units p256_verify_g*.hip)
+#define PBFTV_COMBOS_G29(X) X(29, 24) X(29, 22) X(29, 21) X(29, 20) X(29, 16)
+#define PBFTV_COMBOS_G26(X) X(26, 24) X(26, 22) X(26, 21) X(26, 20) X(26, 16)
+#define PBFTV_COMBOS_G24(X) X(24, 24) X(24, 22) X(24, 20) X(24, 16)
+#define PBFTV_COMBOS_SMALL(X) X(20, 20) X(16, 16) X(16, 12) X(16, 8) X(8, 8)
+#define PBFTV_COMBOS(X) PBFTV_COMBOS_G29(X) PBFTV_COMBOS_G26(X) PBFTV_COMBOS_G24(X) PBFTV_COMBOS_SMALL(X)
 #define PBFTV_TABLE_WIDTHS(X) X(8) X(12) X(16) X(20) X(21) X(22) X(24) X(26) X(29)
 struct TableScratch {
   void* bases;
@@ -58,6 +61,31 @@ hipError_t launch_pack_bits(const uint8_t* okb, uint64_t n, uint8_t* bitmap, hip
 // points, butterfly sum, check) in one launch.  Output: okbytes[i] (one byte per
 // signature) when okbytes != nullptr, else bit i of bitmap set/cleared by word
 // atomics (bitmap need not be zeroed; its word-aligned 4-byte span is touched).
+// argument packs of the per-geometry launchers (verify_kernels.h)
+struct CombArgs {
+  const void* scal;
+  const uint8_t* flag;
+  const uint8_t* sigs;
+  const uint32_t* key_idx;
+  uint64_t n;
+  const uint32_t* gtab;
+  const uint32_t* qtabs;
+  uint8_t* bitmap;
+  const uint32_t* perm;
+  uint8_t* okb;
+};
+struct WaveArgs {
+  const uint8_t* hashes;
+  const uint8_t* sigs;
+  const uint32_t* key_idx;
+  uint64_t n;
+  const uint32_t* key_valid;
+  uint32_t nkeys;
+  const uint32_t* gtab;
+  const uint32_t* qtabs;
+  uint8_t* bitmap;
+  uint8_t* okbytes;
+};
 hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
                              uint64_t n, const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
                              const uint32_t* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st);

@@ -20,6 +20,7 @@
 // (tests/cpp) only.
 #pragma once
 #include "fe29.h"
+#include "fes.h"
 #include "safegcd.h"
 
 namespace pbftv {
@@ -433,27 +434,25 @@ PBFTV_HD bool comb2_mult(jac& acc, const uint32_t u1[8], const uint32_t u2[8], L
 // additions into one XYZZ accumulator (8M + 2S per addition instead of
 // 7M + 4S, and fewer serial carry chains).  Exceptional steps leave ZZ == 0
 // (xyzz_madd), and the caller then reruns the signature with comb2_pass<true>.
-PBFTV_HD void comb_add_entry_xyzz(xyzz& acc, bool& inf, int d, const uint32_t ew[16]) {
+// The table point of digit d (|d| - 1 selects the entry, sign(d) negates y)
+// added to the signed-limb XYZZ accumulator (fes.h); the first point is loaded.
+PBFTV_HD void comb_add_entry_xyzz(xyzz_s& acc, bool& inf, int d, const uint32_t ew[16]) {
   fe x, y;
   entry_to_fe(x, y, ew);
-  if (d < 0) {
-    fe ny;
-    fe_neg_lazy(ny, y);
-    fe_norm(y, ny);
-  }
+  fs_cneg(y, y, d < 0);
   if (inf) {
     acc.x = x;
-    acc.y = y;
+    fs_norm(acc.y, y);
     fe_set(acc.zz, kOneP);
     fe_set(acc.zzz, kOneP);
     inf = false;
     return;
   }
-  xyzz_madd(acc, x, y);
+  xyzz_madd_s(acc, x, y);
 }
 
 template <int WG, int WQ, class LoadG, class LoadQ>
-PBFTV_HD bool comb2_pass_xyzz(xyzz& acc, const uint32_t u1[8], const uint32_t u2[8], LoadG load_g, LoadQ load_q) {
+PBFTV_HD bool comb2_pass_xyzz(xyzz_s& acc, const uint32_t u1[8], const uint32_t u2[8], LoadG load_g, LoadQ load_q) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
   constexpr int nW = nG > nQ ? nG : nQ;
   bool inf = true;
@@ -517,14 +516,42 @@ PBFTV_HD bool ecdsa_check(const xyzz& R, bool finite, const uint32_t r_w[8]) {
   return ecdsa_check_xd(R.x, R.zz, finite, r_w);
 }
 
+// The same test on the signed-limb accumulator (fes.h): X == r ZZ, or
+// X == (r + n) ZZ when r + n < p.
+PBFTV_HD bool ecdsa_check(const xyzz_s& R, bool finite, const uint32_t r_w[8]) {
+  if (!finite) return false;
+  fe rr, r2p, lhs, d;
+  fe_from_words(rr, r_w);
+  fe_set(r2p, kR2P);
+  fs_mul(rr, rr, r2p);        // r in Montgomery form
+  fs_mul(lhs, rr, R.zz);
+  fs_sub(d, lhs, R.x);
+  if (fs_is_zero(d)) return true;
+  if (words_lt(r_w, kPMinusN32)) {  // r + n < p
+    uint32_t rn[8];
+    uint64_t cy = 0;
+    for (int i = 0; i < 8; ++i) {
+      cy += (uint64_t)r_w[i] + kN32[i];
+      rn[i] = (uint32_t)cy;
+      cy >>= 32;
+    }
+    fe_from_words(rr, rn);
+    fs_mul(rr, rr, r2p);
+    fs_mul(lhs, rr, R.zz);
+    fs_sub(d, lhs, R.x);
+    if (fs_is_zero(d)) return true;
+  }
+  return false;
+}
+
 // Whole comb + check for one signature: XYZZ fast pass, complete-addition
 // Jacobian rerun when a step was exceptional (ZZ == 0).
 template <int WG = 8, int WQ = 8, class LoadG, class LoadQ>
 PBFTV_HD bool comb2_verify(const uint32_t u1[8], const uint32_t u2[8], const uint32_t r_w[8], LoadG load_g,
                            LoadQ load_q) {
-  xyzz A;
+  xyzz_s A;
   const bool fin = comb2_pass_xyzz<WG, WQ>(A, u1, u2, load_g, load_q);
-  if (fin && fe_is_zero(A.zz)) {
+  if (fin && fs_is_zero(A.zz)) {
     jac R;
     const bool f2 = comb2_pass<true, WG, WQ>(R, u1, u2, load_g, load_q);
     return ecdsa_check(R, f2, r_w);

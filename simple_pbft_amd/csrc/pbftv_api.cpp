@@ -62,6 +62,10 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
   }
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   template <class T>
   T* as() const {
     return reinterpret_cast<T*>(p);
@@ -88,6 +92,10 @@ struct HostBuf {
     p = nullptr;
     cap = 0;
   }
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
   template <class T>
   T* as() const {
     return reinterpret_cast<T*>(p);
@@ -113,6 +121,12 @@ struct Device {
   // pinned staging for the one H2D and the results
   DevBuf arena, msgok;
   HostBuf mstage, mout;
+  // Device scratch (scal, flag, prefix, ksort, okb, order_scratch) is shared by
+  // calls on d.stream and on caller streams (the *_dev entry points).  The
+  // mutex orders the enqueues; this event orders the execution: a call on a
+  // different stream than the last scratch user first waits for it.
+  hipEvent_t scratch_ev = nullptr;
+  hipStream_t scratch_st = nullptr;
   // kernel timing (events recorded around launches while ctx timing is on)
   const bool* timing = nullptr;
   static constexpr int kKernels = 5;  // PBFTV_K_*
@@ -120,6 +134,21 @@ struct Device {
   double acc_ms[kKernels] = {0, 0, 0, 0, 0};
   uint64_t launches[kKernels] = {0, 0, 0, 0, 0};
 };
+
+// before / after enqueueing work that uses the device scratch on stream st
+hipError_t scratch_acquire(Device& d, hipStream_t st) {
+  if (d.scratch_st != nullptr && d.scratch_st != st) return hipStreamWaitEvent(st, d.scratch_ev, 0);
+  return hipSuccess;
+}
+
+hipError_t scratch_release(Device& d, hipStream_t st) {
+  if (!d.scratch_ev) {
+    hipError_t e = hipEventCreateWithFlags(&d.scratch_ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  d.scratch_st = st;
+  return hipEventRecord(d.scratch_ev, st);
+}
 
 // record start/stop events around one launch when timing is enabled
 template <class F>
@@ -214,6 +243,7 @@ struct Packer {
   std::vector<Seg> segs;
   std::vector<std::vector<uint64_t>> owned;  // rebased offsets, slots (inner buffers stay put when moved)
   size_t total = 0;
+  bool null_blob = false;  // a string column with nonzero lengths but no data pointer
   size_t add(const void* src, size_t bytes) {
     const size_t o = total;
     segs.push_back({src, bytes, o});
@@ -236,6 +266,10 @@ struct Packer {
         b = std::max(b, off[i] + len[i]);
       }
     if (a > b) a = b = 0;
+    if (b > a && data == nullptr) {
+      null_blob = true;
+      a = b = 0;
+    }
     std::vector<uint64_t> r(hi - lo);
     for (uint64_t i = lo; i < hi; ++i) r[i - lo] = len[i] ? off[i] - a : 0;
     Str s;
@@ -248,6 +282,7 @@ struct Packer {
 
 // pinned copy + one H2D into d.arena (stream-ordered before the kernels that read it)
 int upload(Device& d, const Packer& p) {
+  if (p.null_blob) return fail(PBFTV_EINVAL, "string column: nonzero lengths with a null data pointer");
   HIP_TRY(d.mstage.ensure(p.total + 16));
   HIP_TRY(d.arena.ensure(p.total + 16));
   uint8_t* h = d.mstage.as<uint8_t>();
@@ -351,12 +386,12 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
-    for (DevBuf* b : {&d->gtab, &d->qtabs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag, &d->prefix,
-                      &d->bitmap,
-                      &d->data, &d->offsets, &d->lengths, &d->order, &d->order_scratch, &d->digests, &d->expected,
-                      &d->shabits, &d->arena, &d->msgok})
-      b->release();
+    for (DevBuf* b : {&d->gtab, &d->qtabs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag,
+                      &d->prefix, &d->bitmap, &d->ksort, &d->okb, &d->data, &d->offsets, &d->lengths, &d->order,
+                      &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok})
+      b->release();  // explicit, with this device current (the destructors are a backstop)
     for (HostBuf* b : {&d->stage, &d->mstage, &d->mout}) b->release();
+    if (d->scratch_ev) (void)hipEventDestroy(d->scratch_ev);
     (void)hipStreamDestroy(d->stream);
   }
   delete ctx;
@@ -644,6 +679,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   HIP_TRY(d.scal.ensure(n * 64));
   HIP_TRY(d.flag.ensure(n));
   HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
+  HIP_TRY(scratch_acquire(d, st));
   const bool sorted = pbftv::key_sort_wanted(n, d.nkeys);
   if (sorted) {  // comb lanes in key order: a wave's table lookups share keys (p256_kernels.hip k_key_*)
     HIP_TRY(d.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
@@ -661,6 +697,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
                                     sorted ? d.okb.as<uint8_t>() : nullptr, st);
   }));
   if (sorted) HIP_TRY(pbftv::launch_pack_bits(d.okb.as<uint8_t>(), n, d_bitmap, st));
+  HIP_TRY(scratch_release(d, st));
   return PBFTV_OK;
 }
 
@@ -767,7 +804,10 @@ int pbftv_sha256_order_dev(pbftv_ctx* ctx, int dev, const uint32_t* d_lengths, u
   std::lock_guard<std::mutex> lk(d.mu);
   HIP_TRY(hipSetDevice(d.id));
   HIP_TRY(d.order_scratch.ensure(pbftv::sha256_order_scratch_bytes(n)));
-  HIP_TRY(pbftv::launch_sha256_order(d_lengths, n, d_order, d.order_scratch.p, pick_stream(d, stream)));
+  hipStream_t st = pick_stream(d, stream);
+  HIP_TRY(scratch_acquire(d, st));
+  HIP_TRY(pbftv::launch_sha256_order(d_lengths, n, d_order, d.order_scratch.p, st));
+  HIP_TRY(scratch_release(d, st));
   return PBFTV_OK;
 }
 
@@ -815,8 +855,10 @@ static int sha_host(pbftv_ctx* ctx, const uint8_t* data, const uint64_t* offsets
     if (span) HIP_TRY(hipMemcpyAsync(d.data.p, data + lo_b, span, hipMemcpyHostToDevice, d.stream));
     HIP_TRY(hipMemcpyAsync(d.offsets.p, off.data(), m * 8, hipMemcpyHostToDevice, d.stream));
     HIP_TRY(hipMemcpyAsync(d.lengths.p, lengths + s.lo, m * 4, hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(scratch_acquire(d, d.stream));
     HIP_TRY(pbftv::launch_sha256_order(d.lengths.as<uint32_t>(), m, d.order.as<uint32_t>(), d.order_scratch.p,
                                        d.stream));
+    HIP_TRY(scratch_release(d, d.stream));
     uint8_t* dexp = nullptr;
     if (expected) {
       HIP_TRY(d.expected.ensure(m * 32));

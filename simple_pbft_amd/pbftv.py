@@ -491,6 +491,8 @@ class Verifier:
         if sigs is not None:
             sigs = np.ascontiguousarray(sigs, np.uint8)
             key_idx = np.ascontiguousarray(key_idx, np.uint32)
+            if sigs.shape != (n, 64) or key_idx.shape != (n,):
+                raise ValueError("flush_votes: sigs must be (n, 64) uint8 and key_idx (n,)")
             sp, kp = sigs.ctypes.data, key_idx.ctypes.data
         if states is not None:
             sv = np.ascontiguousarray(states[0], np.int64)
@@ -498,6 +500,8 @@ class Verifier:
             sd = np.ascontiguousarray(states[2], np.uint8)
             si = np.ascontiguousarray(state_idx, np.uint32)
             k = len(sv)
+            if sl.shape != (k,) or sd.shape != (k, 32) or si.shape != (n,):
+                raise ValueError("flush_votes: states must be (k,), (k,), (k, 32) and state_idx (n,)")
             svp, slp, sdp, sip = sv.ctypes.data, sl.ctypes.data, sd.ctypes.data, si.ctypes.data
         _check(self._L.pbftv_flush_votes(self._h, n, *cols.args(), sp, kp, k, svp, slp, sdp, sip,
                                          _ptr(out_d), _ptr(sbm), _ptr(mbm)))

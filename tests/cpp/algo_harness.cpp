@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../simple_pbft_amd/csrc/p256_algo.h"
+#include "../../simple_pbft_amd/csrc/fes.h"
 
 using namespace pbftv;
 
@@ -171,6 +172,46 @@ int h_verify_w(int w, const uint8_t* hash, const uint8_t* rs, const uint32_t* gt
   else if (w == 11) run(CombGeom<11>());
   else return -1;
   return ok ? 1 : 0;
+}
+
+// ---- signed-limb arithmetic (fes.h) ----
+void h_fs_mul(const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  fe x, y, z;
+  memcpy(x.v, a, 36); memcpy(y.v, b, 36);
+  fs_mul(z, x, y);
+  memcpy(r, z.v, 36);
+}
+void h_fs_sqr(const uint32_t* a, uint32_t* r) {
+  fe x, z;
+  memcpy(x.v, a, 36);
+  fs_sqr(z, x);
+  memcpy(r, z.v, 36);
+}
+void h_fs_mul2_add(const uint32_t* a, const uint32_t* b, const uint32_t* c, const uint32_t* d, uint32_t* r) {
+  fe x, y, u, v, z;
+  memcpy(x.v, a, 36); memcpy(y.v, b, 36); memcpy(u.v, c, 36); memcpy(v.v, d, 36);
+  fs_mul2_add(z, x, y, u, v);
+  memcpy(r, z.v, 36);
+}
+void h_fs_norm(const uint32_t* a, uint32_t* r) {
+  fe x, z;
+  memcpy(x.v, a, 36);
+  fs_norm(z, x);
+  memcpy(r, z.v, 36);
+}
+void h_fs_canon(const uint32_t* a, uint32_t* r) {
+  fe x, z;
+  memcpy(x.v, a, 36);
+  fs_canon(z, x);
+  memcpy(r, z.v, 36);
+}
+void h_xyzz_madd_s(uint32_t* acc, const uint32_t* pt) {
+  xyzz_s A;
+  fe x, y;
+  memcpy(A.x.v, acc, 36); memcpy(A.y.v, acc + 9, 36); memcpy(A.zz.v, acc + 18, 36); memcpy(A.zzz.v, acc + 27, 36);
+  memcpy(x.v, pt, 36); memcpy(y.v, pt + 9, 36);
+  xyzz_madd_s(A, x, y);
+  memcpy(acc, A.x.v, 36); memcpy(acc + 9, A.y.v, 36); memcpy(acc + 18, A.zz.v, 36); memcpy(acc + 27, A.zzz.v, 36);
 }
 
 // XYZZ mixed addition on raw limbs: acc = x||y||zz||zzz (36 words), pt = x||y (18 words).

@@ -28,7 +28,7 @@ def H():
     d = os.path.join(ROOT, "tests", "cpp")
     so = os.path.join(d, "libalgo_harness.so")
     src = os.path.join(d, "algo_harness.cpp")
-    hdrs = [os.path.join(ROOT, "simple_pbft_amd", "csrc", f) for f in ("fe29.h", "p256_algo.h", "p256_consts.h")]
+    hdrs = [os.path.join(ROOT, "simple_pbft_amd", "csrc", f) for f in ("fe29.h", "fes.h", "p256_algo.h", "p256_consts.h")]
     if not os.path.exists(so) or any(os.path.getmtime(h) > os.path.getmtime(so) for h in hdrs + [src]):
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", so, src], check=True)
     return ctypes.CDLL(so)
@@ -302,3 +302,127 @@ def test_xyzz_madd_chain_values_and_bounds(H):
         a2 = A(*acc)
         H.h_xyzz_madd(a2, Pt(*limbs(mont(x)), *limbs(mont(y))))
         assert val(a2[18:27]) % P == 0 and val(a2[27:36]) % P == 0
+
+
+# ---- signed-limb arithmetic (simple_pbft_amd/csrc/fes.h, the comb's hot loop) ----
+S_BOUND = int(2 ** 257.5)
+D_BOUND = int(2 ** 258.5)
+
+
+def slimbs(l):
+    return (ctypes.c_uint32 * 9)(*[x & 0xFFFFFFFF for x in l])
+
+
+def sval(l):
+    """value of signed 32-bit limbs"""
+    return sum((int(x) - (1 << 32) if int(x) & 0x80000000 else int(x)) << (29 * i) for i, x in enumerate(l))
+
+
+def s_limbs_of(v):
+    """S-type limbs of a (possibly negative) value: limbs 0..7 in [0, 2^29), limb 8 the signed rest"""
+    l = [(v >> (29 * i)) & M29 for i in range(8)]
+    l.append(v >> 232)
+    return l
+
+
+def rand_s(rng, extreme=False):
+    if extreme:
+        v = int(rng.choice([S_BOUND - 1, -S_BOUND + 1, 0, P - 1, -(P - 1)]))
+        l = s_limbs_of(v)
+        if v > 0:
+            l[:8] = [M29] * 8 if rng.integers(0, 2) else l[:8]
+    else:
+        v = int.from_bytes(rng.bytes(33), "big") % (2 * S_BOUND) - S_BOUND
+        l = s_limbs_of(v)
+    while abs(sum(x << (29 * i) for i, x in enumerate(l))) >= S_BOUND:
+        l[8] -= 1 if l[8] > 0 else -1
+    return l, sum(x << (29 * i) for i, x in enumerate(l))
+
+
+def rand_d(rng, extreme=False):
+    a, va = rand_s(rng, extreme)
+    b, vb = rand_s(rng, extreme)
+    d = [x - y for x, y in zip(a, b)]
+    return d, va - vb
+
+
+def check_s(out):
+    v = sval(out)
+    assert all(0 <= int(x) < (1 << 29) for x in out[:8]), list(out)
+    assert abs(v) < S_BOUND, v
+    return v
+
+
+def test_fs_mul_sqr_types_and_values(H):
+    """fs_mul / fs_sqr / fs_mul2_add on S- and D-type inputs, random and at the
+    type bounds: Montgomery product mod p, S-type output, and the output lies
+    in (T / 2^261, T / 2^261 + 1.0001 p) (the 29-bit top digit)."""
+    rng = np.random.default_rng(0x5161)
+    out = (ctypes.c_uint32 * 9)()
+    Rinv = pow(R, -1, P)
+    for it in range(3000):
+        ext = it % 5 == 0
+        kinds = [(rand_s, rand_s), (rand_s, rand_d), (rand_d, rand_d)][it % 3]
+        (la, a), (lb, b) = kinds[0](rng, ext), kinds[1](rng, ext)
+        assert all(abs(x) < (1 << 29) for x in la[:8] + lb[:8])
+        H.h_fs_mul(slimbs(la), slimbs(lb), out)
+        v = check_s(out)
+        assert v % P == a * b * Rinv % P
+        assert a * b / R - 1 < v < a * b / R + 1.0001 * P
+        H.h_fs_sqr(slimbs(lb), out)
+        v = check_s(out)
+        assert v % P == b * b * Rinv % P
+        (lc, c), (ld, d) = rand_d(rng, ext), rand_s(rng, ext)
+        H.h_fs_mul2_add(slimbs(la), slimbs(lb), slimbs(lc), slimbs(ld), out)
+        v = check_s(out)
+        assert v % P == (a * b + c * d) * Rinv % P
+        H.h_fs_canon(slimbs(lc), out)
+        assert val(out) == c % P
+        x = [int(y) for y in rng.integers(-(1 << 30), 1 << 30, 9)]
+        H.h_fs_norm(slimbs(x), out)
+        assert sval(out) == sum(y << (29 * i) for i, y in enumerate(x))
+        assert all(0 <= int(y) < (1 << 29) for y in out[:8])
+
+
+def test_xyzz_madd_s_chain_values_and_bounds(H):
+    """A chain of 200 signed-limb madd-2008-s additions (the comb's step,
+    negative digits as negated y): every intermediate equals the big-integer
+    sum, every accumulator coordinate stays S-type, and adding the
+    accumulator's own point or its negative leaves ZZ == ZZZ == 0."""
+    from oracle import p256
+    rng = np.random.default_rng(71)
+    A = ctypes.c_uint32 * 36
+    Pt = ctypes.c_uint32 * 18
+
+    def mont(v):
+        return v * R % P
+
+    def unmont(v):
+        return v * pow(R, -1, P) % P
+
+    def from_acc(acc):
+        x, y, zz, zzz = (unmont(sval(acc[9 * k:9 * k + 9]) % P) for k in range(4))
+        assert zz != 0 and zzz != 0
+        return x * pow(zz, -1, P) % P, y * pow(zzz, -1, P) % P
+
+    cur = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+    z = int(rng.integers(2, 2 ** 62))
+    acc = A(*[w for v in (mont(cur[0] * z * z % P), mont(cur[1] * z ** 3 % P), mont(z * z % P), mont(z ** 3 % P))
+              for w in limbs(v)])
+    for step in range(200):
+        q = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+        neg = step % 2 == 1
+        ly = [(-x) & 0xFFFFFFFF if neg else x for x in limbs(mont(q[1]))]
+        H.h_xyzz_madd_s(acc, Pt(*limbs(mont(q[0])), *ly))
+        if neg:
+            q = (q[0], (P - q[1]) % P)
+        cur = p256.point_add(cur, q)
+        assert from_acc(acc) == cur, step
+        for k in range(4):
+            check_s(acc[9 * k:9 * k + 9])
+    for neg in (False, True):
+        x, y = from_acc(acc)
+        y = (P - y) % P if neg else y
+        a2 = A(*acc)
+        H.h_xyzz_madd_s(a2, Pt(*limbs(mont(x)), *limbs(mont(y))))
+        assert sval(a2[18:27]) % P == 0 and sval(a2[27:36]) % P == 0

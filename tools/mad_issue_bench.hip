@@ -31,6 +31,22 @@
 #define X1(i) "v_mad_u64_u32 %[x" #i "], s[40:41], %[a], %[b], %[x" #i "]\n\tv_add_u32 %[y" #i "], %[y" #i "], %[a]\n\t"
 #define BODY_MIX X1(0) X1(1) X1(2) X1(3) X1(4) X1(5) X1(6) X1(7)
 
+#define I1(i) "v_mad_i64_i32 %[x" #i "], s[40:41], %[a], %[b], %[x" #i "]\n\t"
+#define BODY_SIGNED I1(0) I1(1) I1(2) I1(3) I1(4) I1(5) I1(6) I1(7) I1(8) I1(9) I1(10) I1(11) I1(12) I1(13) I1(14) I1(15)
+#define N1(i) "v_not_b32 %[y" #i "], %[y" #i "]\n\t"
+#define BODY_NOT N1(0) N1(1) N1(2) N1(3) N1(4) N1(5) N1(6) N1(7) N1(0) N1(1) N1(2) N1(3) N1(4) N1(5) N1(6) N1(7)
+
+#define AB1(i) "v_alignbit_b32 %[y" #i "], %[y" #i "], %[a], 7\n\t"
+#define BODY_ALIGNBIT AB1(0) AB1(1) AB1(2) AB1(3) AB1(4) AB1(5) AB1(6) AB1(7) AB1(0) AB1(1) AB1(2) AB1(3) AB1(4) AB1(5) AB1(6) AB1(7)
+#define B31(i) "v_bitop3_b32 %[y" #i "], %[y" #i "], %[a], %[b] bitop3:0x96\n\t"
+#define BODY_BITOP3 B31(0) B31(1) B31(2) B31(3) B31(4) B31(5) B31(6) B31(7) B31(0) B31(1) B31(2) B31(3) B31(4) B31(5) B31(6) B31(7)
+#define AD3(i) "v_add3_u32 %[y" #i "], %[y" #i "], %[a], %[b]\n\t"
+#define BODY_ADD3 AD3(0) AD3(1) AD3(2) AD3(3) AD3(4) AD3(5) AD3(6) AD3(7) AD3(0) AD3(1) AD3(2) AD3(3) AD3(4) AD3(5) AD3(6) AD3(7)
+#define AND1(i) "v_and_b32 %[y" #i "], %[y" #i "], %[a]\n\t"
+#define BODY_AND AND1(0) AND1(1) AND1(2) AND1(3) AND1(4) AND1(5) AND1(6) AND1(7) AND1(0) AND1(1) AND1(2) AND1(3) AND1(4) AND1(5) AND1(6) AND1(7)
+#define ASH(i) "v_ashrrev_i64 %[x" #i "], 29, %[x" #i "]\n\t"
+#define BODY_ASHR64 ASH(0) ASH(1) ASH(2) ASH(3) ASH(4) ASH(5) ASH(6) ASH(7) ASH(8) ASH(9) ASH(10) ASH(11) ASH(12) ASH(13) ASH(14) ASH(15)
+
 #define OPS_X [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [x4] "+v"(x[4]), [x5] "+v"(x[5]), \
   [x6] "+v"(x[6]), [x7] "+v"(x[7]), [x8] "+v"(x[8]), [x9] "+v"(x[9]), [x10] "+v"(x[10]), [x11] "+v"(x[11]), \
   [x12] "+v"(x[12]), [x13] "+v"(x[13]), [x14] "+v"(x[14]), [x15] "+v"(x[15])
@@ -39,9 +55,10 @@
   [z4] "+v"(z[4]), [z5] "+v"(z[5]), [z6] "+v"(z[6]), [z7] "+v"(z[7])
 #define CLOB "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "vcc"
 
-enum { SAMEC, ROTC, CHAIN, LSHL, ADD, ADDC, MIX, NV };
+enum { SAMEC, ROTC, CHAIN, LSHL, ADD, ADDC, MIX, SIGNED, NOT, ALIGNBIT, BITOP3, ADD3, AND, ASHR64, NV };
 static const char* kName[NV] = {"mad_u64 16 indep, one sdst", "mad_u64 16 indep, 8 sdst rot", "mad_u64 dep chain",
-                                "lshl_add_u64 indep", "add_u32 indep", "add_co+addc pairs", "mad_u64 + add_u32 alt"};
+                                "lshl_add_u64 indep", "add_u32 indep", "add_co+addc pairs", "mad_u64 + add_u32 alt", "mad_i64_i32 16 indep", "not_b32 indep", "alignbit_b32 (VOP3)", "bitop3_b32 (VOP3)",
+                                "add3_u32 (VOP3)", "and_b32 (VOP2)", "ashrrev_i64"};
 
 template <int V>
 __global__ void __launch_bounds__(256) kb(uint32_t* out, int iters, uint32_t seed) {
@@ -60,6 +77,13 @@ __global__ void __launch_bounds__(256) kb(uint32_t* out, int iters, uint32_t see
     if constexpr (V == ADD) asm volatile(BODY_ADD : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
     if constexpr (V == ADDC) asm volatile(BODY_ADDC : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
     if constexpr (V == MIX) asm volatile(BODY_MIX : OPS_X, OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == SIGNED) asm volatile(BODY_SIGNED : OPS_X : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == NOT) asm volatile(BODY_NOT : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == ALIGNBIT) asm volatile(BODY_ALIGNBIT : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == BITOP3) asm volatile(BODY_BITOP3 : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == ADD3) asm volatile(BODY_ADD3 : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == AND) asm volatile(BODY_AND : OPS_Y : [a] "v"(a), [b] "v"(b) : CLOB);
+    if constexpr (V == ASHR64) asm volatile(BODY_ASHR64 : OPS_X : [a] "v"(a), [b] "v"(b) : CLOB);
   }
   uint32_t r = 0;
   for (int j = 0; j < 16; ++j) r ^= (uint32_t)x[j] ^ (uint32_t)(x[j] >> 32);
@@ -101,6 +125,13 @@ int main() {
     run<ADD>(out, w);
     run<ADDC>(out, w);
     run<MIX>(out, w);
+    run<SIGNED>(out, w);
+    run<NOT>(out, w);
+    run<ALIGNBIT>(out, w);
+    run<BITOP3>(out, w);
+    run<ADD3>(out, w);
+    run<AND>(out, w);
+    run<ASHR64>(out, w);
   }
   return 0;
 }

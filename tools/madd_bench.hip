@@ -9,6 +9,7 @@
 #include <cstdlib>
 
 #include "p256_algo.h"
+#include "fes.h"
 
 using namespace pbftv;
 
@@ -36,6 +37,15 @@ __global__ void __launch_bounds__(256, WAVES) kbench(const uint4* __restrict__ t
       jac_madd<false>(acc, ex, ey);
     }
     for (int l = 0; l < 9; ++l) out[lane * 9 + l] = acc.x.v[l] ^ acc.z.v[l] ^ acc.y.v[l];
+  } else if constexpr (V == 2) {
+    xyzz_s acc;
+    acc.x = x; acc.y = y; fe_set(acc.zz, kOneP); fe_set(acc.zzz, kOneP);
+    for (int i = 0; i < iters; ++i) {
+      fe ex, ey;
+      ld_entry(tab, lane + 7 * i + 1, ex, ey);
+      xyzz_madd_s(acc, ex, ey);
+    }
+    for (int l = 0; l < 9; ++l) out[lane * 9 + l] = acc.x.v[l] ^ acc.zz.v[l] ^ acc.y.v[l] ^ acc.zzz.v[l];
   } else {
     xyzz acc;
     acc.x = x; acc.y = y; fe_set(acc.zz, kOneP); fe_set(acc.zzz, kOneP);
@@ -89,5 +99,9 @@ int main() {
   run<1, 2>("madd-2008-s xyzz", tab, out, blocks, iters);
   run<1, 3>("madd-2008-s xyzz", tab, out, blocks, iters);
   run<1, 4>("madd-2008-s xyzz", tab, out, blocks, iters);
+  run<2, 1>("madd-2008-s xyzz signed", tab, out, blocks, iters);
+  run<2, 2>("madd-2008-s xyzz signed", tab, out, blocks, iters);
+  run<2, 3>("madd-2008-s xyzz signed", tab, out, blocks, iters);
+  run<2, 4>("madd-2008-s xyzz signed", tab, out, blocks, iters);
   return 0;
 }
