@@ -168,46 +168,85 @@ def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int):
     return float(np.percentile(ts, 50) * 1e6), float(np.percentile(ts, 99) * 1e6)
 
 
-def cpu_baseline(pub, H, S, K, sample: int):
-    """Oracle port (oracle/p256_ref.c, Go crypto/ecdsa restatement) on host threads."""
-    so = os.path.join(ROOT, "oracle", "liboracle.so")
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_verify(so_name, fn_name, pub, H, S, K, sample: int):
+    so = os.path.join(ROOT, "oracle", so_name)
     if not os.path.exists(so):
         return None
     L = ctypes.CDLL(so)
     vp = ctypes.c_void_p
-    L.oracle_ecdsa_p256_verify_batch.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_int]
+    fn = getattr(L, fn_name)
+    fn.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_int]
     threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 cores
     h, s, k = (np.ascontiguousarray(a[:sample]) for a in (H, S, K))
     bm = np.zeros((sample + 7) // 8, np.uint8)
     t0 = time.perf_counter()
-    L.oracle_ecdsa_p256_verify_batch(h.ctypes.data, s.ctypes.data, k.ctypes.data, sample, pub.ctypes.data, len(pub),
-                                     bm.ctypes.data, threads)
+    fn(h.ctypes.data, s.ctypes.data, k.ctypes.data, sample, pub.ctypes.data, len(pub), bm.ctypes.data, threads)
     dt = time.perf_counter() - t0
-    return {"value": sample / dt, "unit": "verifies/s", "cores": threads, "kind": "port",
-            "sample": f"first {sample} signatures of the config-4 batch (oracle/p256_ref.c, {threads} pthreads)",
-            "_bitmap": bm}
+    return {"value": sample / dt, "unit": "verifies/s", "cores": threads, "nproc": os.cpu_count(),
+            "cpu_model": cpu_model(), "_bitmap": bm}
 
 
 def openssl_standin(pub, H, S, K, sample: int):
-    """OpenSSL 3 libcrypto ECDSA_do_verify on host threads (SURVEY.md §8(d)(ii)
-    stand-in for Go crypto/ecdsa; oracle/openssl_standin.c)."""
-    so = os.path.join(ROOT, "oracle", "libopenssl_standin.so")
-    if not os.path.exists(so):
-        return None
-    L = ctypes.CDLL(so)
-    vp = ctypes.c_void_p
-    L.standin_ecdsa_p256_verify_batch.restype = ctypes.c_int64
-    L.standin_ecdsa_p256_verify_batch.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_int]
-    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 cores
-    h, s, k = (np.ascontiguousarray(a[:sample]) for a in (H, S, K))
-    bm = np.zeros((sample + 7) // 8, np.uint8)
-    t0 = time.perf_counter()
-    L.standin_ecdsa_p256_verify_batch(h.ctypes.data, s.ctypes.data, k.ctypes.data, sample, pub.ctypes.data, len(pub),
-                                      bm.ctypes.data, threads)
-    dt = time.perf_counter() - t0
-    return {"value": sample / dt, "unit": "verifies/s", "cores": threads,
-            "sample": f"first {sample} signatures of the config-4 batch (oracle/openssl_standin.c, {threads} pthreads,"
-                      " OpenSSL 3 nistz256)", "_bitmap": bm}
+    """cpu_baseline: OpenSSL 3 libcrypto ECDSA_do_verify on host threads
+    (oracle/openssl_standin.c).  Go 1.19's amd64 P-256
+    (crypto/elliptic p256_asm) is a port of OpenSSL's nistz256 assembly, so this
+    is the faithful stand-in for the reference's CPU verify path, which cannot
+    run here (no Go toolchain)."""
+    r = _cpu_verify("libopenssl_standin.so", "standin_ecdsa_p256_verify_batch", pub, H, S, K, sample)
+    if r is not None:
+        r["kind"] = "openssl_standin"
+        r["sample"] = (f"first {sample} signatures of the config-4 batch (oracle/openssl_standin.c, {r['cores']} "
+                       "pthreads, OpenSSL 3 nistz256)")
+    return r
+
+
+def cpu_oracle_port(pub, H, S, K, sample: int):
+    """The oracle port (oracle/p256_ref.c: 4x64-bit CIOS, bit-serial Shamir --
+    deliberately simple, for parity) on host threads; reported beside the
+    stand-in, not as the baseline."""
+    r = _cpu_verify("liboracle.so", "oracle_ecdsa_p256_verify_batch", pub, H, S, K, sample)
+    if r is not None:
+        r["kind"] = "port"
+        r["sample"] = f"first {sample} signatures of the config-4 batch (oracle/p256_ref.c, {r['cores']} pthreads)"
+    return r
+
+
+def host_path(ver, H, S, K, ok, reps=5):
+    """pbftv_ecdsa_p256_verify_batch on the full batch from host memory: the
+    drop-in path a pool flush would call (PCIe in, bitmap out), pipelined in
+    chunks (pbftv_api.cpp verify_host_pipelined).  Pageable numpy inputs (staged
+    through pinned memory by parallel memcpy) and pinned inputs (pbftv_host_alloc:
+    DMA straight from the caller's buffers).  Best-of wall time."""
+    n = len(K)
+    res = {}
+    for label, arrays in (("pageable", (H, S, K)), ("pinned", None)):
+        pins = None
+        if arrays is None:
+            pins = [ver.pinned(a) for a in (H, S, K)]
+            arrays = tuple(p.a for p in pins)
+        got = ver.verify_batch(*arrays)
+        good = bool((got == ok).all())
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ver.verify_batch(*arrays)
+            ts.append(time.perf_counter() - t0)
+        res[label] = {"verifies_per_s": n / min(ts), "ms": min(ts) * 1e3, "check": good}
+        if pins:
+            for p in pins:
+                p.free()
+    return res
 
 
 # ---------------------------------------------------------------- other BASELINE configs
@@ -285,8 +324,30 @@ def run_certs(ver, n_keys, per_cert, n_certs, pool_certs, label):
 
 def run_config5(ver, n=1_000_000, steps=5):
     """configs[4]: SHA-256 over 1M messages of 256 B..4 KiB (digest kernel alone)."""
-    import hashlib
     data, off, ln = synth.sha_config5(n)
+    return _sha_run(ver, data, off, ln, steps, "config5: SHA-256 of {n} messages, {lens} B, {gb:.2f} GB, {blocks} blocks")
+
+
+def run_sha_pbft(ver, n=1_000_000, steps=5):
+    """The digests utils.Hash actually computes (utils/utils.go:13-17 via
+    digest(), pbft_impl.go:235-243): Go-JSON preimages of 99-244 B -- RequestMsg
+    99 B (2 blocks), ReplyMsg 110 B (2), VoteMsg 167 B (3), PrePrepareMsg 244 B
+    (4) -- in the reference's per-request mix (1 request : 3
+    pre-prepares : 21 votes : 4 replies)."""
+    rng = np.random.default_rng(0x50424655)
+    kinds = np.array([99, 244, 167, 110])
+    ln = kinds[rng.choice(4, size=n, p=np.array([1, 3, 21, 4]) / 29.0)].astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    data = rng.integers(32, 127, int(ln.sum()), dtype=np.uint8)
+    return _sha_run(ver, data, off, ln, steps,
+                    "PBFT digests: SHA-256 of {n} Go-JSON-sized messages, {lens} B (request/pre-prepare/vote/reply "
+                    "mix), {gb:.2f} GB, {blocks} blocks")
+
+
+def _sha_run(ver, data, off, ln, steps, label):
+    import hashlib
+    n = len(ln)
     dd = ver.to_device(0, data, pad=64)
     do, dl = ver.to_device(0, off), ver.to_device(0, ln)
     dord, dg = ver.alloc(0, 4 * n), ver.alloc(0, 32 * n)
@@ -307,7 +368,7 @@ def run_config5(ver, n=1_000_000, steps=5):
     for b in (dd, do, dl, dord, dg):
         b.free()
     ops = blocks * SHA_OPS_PER_BLOCK
-    return {"workload": f"config5: SHA-256 of {n} messages, {lo_hi(ln)} B, {total / 1e9:.2f} GB, {blocks} blocks",
+    return {"workload": label.format(n=n, lens=lo_hi(ln), gb=total / 1e9, blocks=blocks),
             "digests_per_s": n / best, "GB_per_s": total / best / 1e9, "ms": best * 1e3, "kernel_ms": kavg * 1e3,
             "roofline": {"bound": "valu", "achieved": ops / kavg / 1e12, "peak": VALU_PEAK / 1e12,
                          "unit": "T VALU ops/s (1528 per 64-B block, SURVEY §8(d))",
@@ -324,19 +385,41 @@ SHA_OPS_PER_BLOCK = 1528
 VALU_PEAK = 256 * 4 * 32 * 2.4e9   # full-rate 32-bit VALU: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
 
 
+PMC_JSON = os.path.join(ROOT, "profiles", "r02_pmc.json")
+
+
+def pmc_figures(kernel: str, geometry):
+    """Counter-derived figures of one kernel from the committed PMC summary
+    (tools/pmc_passes.sh + tools/pmc_summary.py); the comb's only when the
+    summary was measured at the same table geometry."""
+    if not os.path.exists(PMC_JSON):
+        return {}
+    with open(PMC_JSON) as f:
+        pm = json.load(f).get("kernels", {})
+    e = pm.get(kernel, {})
+    if kernel == "ecdsa_comb" and e.get("geometry") != list(geometry):
+        return {}
+    keep = ("valu_issue_frac", "valu_busy_frac", "valu_insts_per_wave", "hbm_bytes_per_launch", "clock_ghz",
+            "kernel_ms")
+    return {k: e[k] for k in keep if k in e}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per rank")
+    ap.add_argument("--n", type=int, default=1 << 20,
+                    help="global batch (strong scaling, the default: BASELINE configs[3] shards N/k over k GPUs); "
+                         "with --weak: signatures per rank")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: every rank verifies its own --n batch")
     ap.add_argument("--keys", type=int, default=100)
-    ap.add_argument("--no-extras", action="store_true", help="skip QC latency and CPU baseline")
+    ap.add_argument("--no-extras", action="store_true", help="skip QC latency, host path, CPU baselines, other configs")
     ap.add_argument("--sha-only", action="store_true", help="only configs[4] (SHA-256 digest kernel), one JSON line")
     args = ap.parse_args()
     if args.sha_only:
         ver = Verifier(device_mask=1)
-        print(json.dumps(run_config5(ver)), flush=True)
+        print(json.dumps({"config5": run_config5(ver), "pbft_digests": run_sha_pbft(ver)}), flush=True)
         ver.close()
         return
 
@@ -346,16 +429,28 @@ def main():
     # (only to rehearse the N > 1 flow on a 1-GPU box -- not a scaling number)
     share = os.environ.get("PBFTV_BENCH_SHARE_DEVICE") == "1"
     ver = Verifier(device_mask=1 if share else 1 << local)
-    n = args.n
-    pub, H, S, K, ok = synth.config4(n, n_keys=args.keys, seed=0x50424654 + rank)
+    if args.weak:
+        n_global, lo = args.n * ws, 0
+        n = args.n
+        pub, H, S, K, ok = synth.config4(n, n_keys=args.keys, seed=0x50424654 + rank)
+    else:
+        # strong scaling: the one global batch, contiguous shards of whole 512-signature groups
+        n_global = args.n
+        per = -(-n_global // ws)
+        per = -(-per // 512) * 512
+        lo, hi = min(n_global, rank * per), min(n_global, (rank + 1) * per)
+        n = hi - lo
+        pub, H, S, K, ok = synth.config4(n_global, n_keys=args.keys, seed=0x50424654)
+        H, S, K, ok = H[lo:hi], S[lo:hi], K[lo:hi], ok[lo:hi]
     valid = ver.register_keys(pub)
     assert valid.all()
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
-    db = ver.alloc(0, (n + 7) // 8)
+    db = ver.alloc(0, (n + 7) // 8 + 1)
     ver.reserve(n)
 
     def step():
-        ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
+        if n:
+            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
 
     for _ in range(args.warmup):
         step()
@@ -378,17 +473,20 @@ def main():
     ver.set_kernel_timing(False)
     t_max = d.max(elapsed)
     all_ok = d.sum(0.0 if check else 1.0) == 0.0
-    total = n * ws * args.steps
+    total = n_global * args.steps
     value = total / t_max
 
+    mode = "weak" if args.weak else "strong"
     out = {
         "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": ws, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "scaling": mode, "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (OpenSSL-signed P-256 votes, tools/synth.py)",
-        "config": {"workload": f"config4: {n} ECDSA-P256 sigs per rank, {args.keys}-key table, 1% corrupted "
-                               "(8 classes)", "global_batch": n * ws, "keys": args.keys,
-                   "parallelism": f"shard{ws} (independent per-GPU batches, no collective)"},
+        "config": {"workload": (f"config4: {n_global} ECDSA-P256 sigs" +
+                                (f" ({args.n} per rank)" if args.weak else f" sharded N/{ws}") +
+                                f", {args.keys}-key table, 1% corrupted (8 classes)"),
+                   "global_batch": n_global, "keys": args.keys,
+                   "parallelism": f"shard{ws} ({mode} scaling: independent per-GPU shards, no collective)"},
         "check": "pass" if all_ok else "FAIL",
     }
     if rank == 0:
@@ -400,43 +498,44 @@ def main():
         mc = macs_comb(gb, qb)
         kern = {
             "ecdsa_comb": {"avg_ms": comb_avg * 1e3, "macs_per_verify": mc, "window_bits": [gb, qb],
-                           "achieved_tmacs": n * mc / comb_avg / 1e12},
+                           "achieved_tmacs": n * mc / max(comb_avg, 1e-12) / 1e12},
             "ecdsa_scalars": {"avg_ms": scal_avg * 1e3, "macs_per_verify": ms, "sigs_per_lane": kb,
-                              "achieved_tmacs": n * ms / scal_avg / 1e12},
+                              "achieved_tmacs": n * ms / max(scal_avg, 1e-12) / 1e12},
         }
         dom = "ecdsa_comb" if comb_avg >= scal_avg else "ecdsa_scalars"
         ach = kern[dom]["achieved_tmacs"]
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-        if os.path.exists(pmc):  # PMC passes of the same workload (tools/pmc_passes.sh), same table geometry only
-            with open(pmc) as f:
-                pm = json.load(f)
-            if pm.get("ecdsa_comb", {}).get("geometry") == [gb, qb]:
-                traffic = pm.get(dom, {}).get("hbm_bytes_per_launch")
+        pmc = pmc_figures(dom, (gb, qb))
         out["roofline"] = {"bound": "valu", "kernel": dom, "achieved": ach, "peak": MAD_PEAK / 1e12,
-                           "unit": "TMAC/s (v_mad_u64_u32 limb MACs)", "frac": ach * 1e12 / MAD_PEAK,
-                           "traffic": traffic}
+                           "unit": "TMAC/s (v_mad limb MACs)", "frac": ach * 1e12 / MAD_PEAK,
+                           "traffic": pmc.get("hbm_bytes_per_launch"),
+                           "valu_issue_frac": pmc.get("valu_issue_frac"),
+                           "valu_busy_frac": pmc.get("valu_busy_frac"),
+                           "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
+                           "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc else None}
         out["kernels"] = kern
         out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
         if not args.no_extras and ws == 1:
+            out["host_path"] = host_path(ver, H, S, K, ok)
+            out["host_path_verifies_per_s"] = out["host_path"]["pageable"]["verifies_per_s"]
             p50_4, p99_4 = qc_latency(ver, 4, 3, 2000, 11)
             p50_100, p99_100 = qc_latency(ver, 100, 67, 1000, 12)
             out["qc_latency_us"] = {"p50_n4_3sigs": p50_4, "p99_n4_3sigs": p99_4, "p50_n100_67sigs": p50_100,
                                     "p99_n100_67sigs": p99_100,
                                     "definition": "host submit -> accept bitmap + quorum on host, pbftv_qc_verify"}
-            cb = cpu_baseline(pub, H, S, K, sample=32768)
+            sample = 262144
+            cb = openssl_standin(pub, H, S, K, sample=sample)
             if cb is not None:
                 bm = cb.pop("_bitmap")
-                cpu_bits = np.unpackbits(bm, bitorder="little")[:32768].astype(bool)
-                cb["agrees_with_gpu"] = bool((cpu_bits == got[:32768]).all())
+                cb["agrees_with_gpu"] = bool((np.unpackbits(bm, bitorder="little")[:sample].astype(bool) ==
+                                              got[:sample]).all())
                 out["cpu_baseline"] = cb
                 out["gpu_vs_cpu"] = value / cb["value"]
-            ost = openssl_standin(pub, H, S, K, sample=131072)
-            if ost is not None:
-                bm = ost.pop("_bitmap")
-                ost["agrees_with_gpu"] = bool((np.unpackbits(bm, bitorder="little")[:131072].astype(bool) ==
-                                               got[:131072]).all())
-                out["cpu_openssl_standin"] = ost
+            port = cpu_oracle_port(pub, H, S, K, sample=32768)
+            if port is not None:
+                bm = port.pop("_bitmap")
+                port["agrees_with_gpu"] = bool((np.unpackbits(bm, bitorder="little")[:32768].astype(bool) ==
+                                                got[:32768]).all())
+                out["cpu_oracle_port"] = port
             out["other_configs"] = {
                 "config1": run_config1(ver),
                 "config2": run_certs(ver, 4, 3, 20000, 4000,
@@ -444,6 +543,7 @@ def main():
                 "config3": run_certs(ver, 100, 67, 10000, 500,
                                      "config3: n=100 committee, 10k certificates x 67 sigs = 670k on one GPU"),
                 "config5": run_config5(ver),
+                "pbft_digests": run_sha_pbft(ver),
             }
         print(json.dumps(out), flush=True)
     for b in (dh, ds, dk, db):

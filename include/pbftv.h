@@ -72,12 +72,23 @@ int pbftv_reserve(pbftv_ctx* ctx, uint64_t n);
  * device's stream (synchronous), and a stream synchronise. */
 int pbftv_dev_alloc(pbftv_ctx* ctx, int dev, uint64_t bytes, void** out_ptr);
 int pbftv_dev_free(pbftv_ctx* ctx, int dev, void* ptr);
+/* Pinned host memory (hipHostMalloc, portable): batches placed in it skip the
+ * staging copy of the host-buffer verify path (e.g. a cgo shim's pool-flush
+ * buffers). */
+int pbftv_host_alloc(pbftv_ctx* ctx, uint64_t bytes, void** out_ptr);
+int pbftv_host_free(pbftv_ctx* ctx, void* ptr);
 int pbftv_memcpy_h2d(pbftv_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes);
 int pbftv_memcpy_d2h(pbftv_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes);
 int pbftv_memset_dev(pbftv_ctx* ctx, int dev, void* dst, int value, uint64_t bytes);
 /* The context's stream of device dev as a hipStream_t (for *_dev calls). */
 void* pbftv_stream(pbftv_ctx* ctx, int dev);
 int pbftv_stream_sync(pbftv_ctx* ctx, int dev);
+/* Caller streams on device dev for *_dev calls (non-blocking HIP streams).  Device
+ * scratch shared by calls on different streams is ordered by the library (an
+ * event per device), so concurrent *_dev calls on several streams are safe. */
+int pbftv_stream_create(pbftv_ctx* ctx, int dev, void** out_stream);
+int pbftv_stream_destroy(pbftv_ctx* ctx, int dev, void* stream);
+int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every
  * kernel launch while enabled.  kernel: 0 = ecdsa scalars, 1 = ecdsa comb,
@@ -233,7 +244,14 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
 int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uint64_t* out_table_bytes);
 
 /* Verify n signatures: hashes (n*32), sig_rs (n*64: r||s big-endian),
- * key_idx (n, index into the registered table).  out_bitmap: ceil(n/8) B. */
+ * key_idx (n, index into the registered table).  out_bitmap: ceil(n/8) B.
+ * Batches up to 2048 signatures take the one-launch latency path (inputs read
+ * by the kernel straight from pinned memory).  Larger batches are split into
+ * one shard per device and each shard is pipelined in chunks: staging copy
+ * (parallel memcpy into pinned memory; skipped when all three input buffers
+ * come from pbftv_host_alloc or are otherwise pinned) -> DMA -> verify, two
+ * chunks in flight (PBFTV_HOST_CHUNK, default 262144 signatures;
+ * PBFTV_COPY_THREADS staging threads, default min(8, host threads - 1)). */
 int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs,
                                   const uint32_t* key_idx, uint64_t n, uint8_t* out_bitmap);
 

@@ -38,21 +38,24 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nbases);
 // valid[key] written for every key built.
 hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g,
                                uint32_t* valid, uint32_t* tables, TableScratch& sc, hipStream_t st);
-size_t ecdsa_scratch_bytes(uint64_t n);
-// stage 1: scal (n * 64 B) + flag (n B) + prefix (scalar_prefix_bytes(n)) device scratch
+// stage 1 -> stage 2 records (verify_kernels.h SigRec: 128 B per signature) and
+// the prefix-product scratch of stage 1's batched inversion
+size_t ecdsa_record_bytes(uint64_t n);
 int scalar_batch(uint64_t n);
 size_t scalar_prefix_bytes(uint64_t n);
+// stage 1: inputs in arrival order; record of signature i written at pos[i]
+// (key order) or at i (pos == nullptr)
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
-                                const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, void* prefix,
-                                const uint32_t* perm, hipStream_t st);
-// stage 2: (wg, wq) one of PBFTV_COMBOS; qtabs = nkeys tables of width wq;
-// bitmap ceil(n/8) B
-hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* flag, const uint8_t* sigs,
-                             const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
-                             uint8_t* bitmap, const uint32_t* perm, uint8_t* okb, hipStream_t st);
-// stage 0 (optional): key order perm[p] = signature at position p sorted by key
-// (scratch: key_sort_scratch_bytes, perm first); with a perm the comb writes
-// okb[i] (n B) and launch_pack_bits builds the bitmap.
+                                const uint32_t* key_valid, uint32_t nkeys, void* rec, void* prefix,
+                                const uint32_t* pos, hipStream_t st);
+// stage 2: (wg, wq) one of PBFTV_COMBOS; qtabs = nkeys tables of width wq.
+// okb == nullptr: records in arrival order, LSB-first bitmap (ceil(n/8) B)
+// written directly; else one byte per signature at its batch index (okb, n B)
+// and launch_pack_bits builds the bitmap.
+hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
+                             uint8_t* bitmap, uint8_t* okb, hipStream_t st);
+// stage 0 (optional): key order pos[i] = position of signature i sorted by key
+// (scratch: key_sort_scratch_bytes, pos first).
 bool key_sort_wanted(uint64_t n, uint32_t nkeys);
 size_t key_sort_scratch_bytes(uint64_t n, uint32_t nkeys);
 hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, hipStream_t st);
@@ -63,15 +66,11 @@ hipError_t launch_pack_bits(const uint8_t* okb, uint64_t n, uint8_t* bitmap, hip
 // atomics (bitmap need not be zeroed; its word-aligned 4-byte span is touched).
 // argument packs of the per-geometry launchers (verify_kernels.h)
 struct CombArgs {
-  const void* scal;
-  const uint8_t* flag;
-  const uint8_t* sigs;
-  const uint32_t* key_idx;
+  const void* rec;
   uint64_t n;
   const uint32_t* gtab;
   const uint32_t* qtabs;
   uint8_t* bitmap;
-  const uint32_t* perm;
   uint8_t* okb;
 };
 struct WaveArgs {

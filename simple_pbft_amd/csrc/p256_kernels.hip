@@ -205,25 +205,26 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
 }
 
 // ---------------------------------------------------------------------------
-// stage 1: scalars.  scal[i] = {u1[8], u2[8]} (LE words); flag[i] = 1 if the
-// signature passes Go's range checks and names a valid registered key.
+// stage 1: scalars.  One 128-B record per signature (SigRec, verify_kernels.h):
+// u1 = e w, u2 = r w (LE words), r, the key index, the signature's batch
+// index and ok = Go's range checks passed and the key is registered and valid.
 //
-// Each lane owns K signatures i = lane + j*L (j < K, L = lanes in the grid, so
-// every load/store is coalesced across the wave) and inverts all K values of s
-// with ONE Fermat inversion (Montgomery's trick): prefix products
-// c_j = s_0 ... s_j go to a limb-major scratch, inv = c_{K-1}^-1, then walking
-// back w_j = inv * c_{j-1}, inv *= s_j.  Per signature that is 7 Montgomery
-// multiplies + 292/K for the inversion instead of 292 + 4.
+// Inputs are read in ARRIVAL order -- each lane owns K signatures i = lane +
+// j*L (j < K, L = lanes in the grid), so every input load is coalesced across
+// the wave -- and each record is written to the signature's position in key
+// order, pos[i] (k_key_scatter; identity without a key order): one full
+// 128-B line per lane, so the comb reads its lane's record coalesced and never
+// gathers through a permutation.  The K values of s share ONE inversion
+// (Montgomery's trick: prefix products c_j = s_0 ... s_j in a limb-major
+// scratch, inv = c_{K-1}^-1, then walking back w_j = inv * c_{j-1},
+// inv *= s_j): per signature 7 Montgomery multiplies + 1/K of a safegcd.
 template <int K>
 __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict__ hashes,
                                                        const uint8_t* __restrict__ sigs,
                                                        const uint32_t* __restrict__ key_idx, uint64_t n,
                                                        const uint32_t* __restrict__ key_valid, uint32_t nkeys,
-                                                       uint4* __restrict__ scal, uint8_t* __restrict__ flag,
-                                                       uint32_t* __restrict__ prefix,
-                                                       const uint32_t* __restrict__ perm) {
-  // outputs at position i; inputs of signature src(i) = perm[i] in key order (k_key_*)
-  auto src = [&](uint64_t i) -> uint64_t { return perm != nullptr ? (uint64_t)perm[i] : i; };
+                                                       SigRec* __restrict__ rec, uint32_t* __restrict__ prefix,
+                                                       const uint32_t* __restrict__ pos) {
   const uint64_t L = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   fe r2n, acc;
@@ -236,7 +237,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     bool ok = false;
     if (i < n) {
       uint32_t s[8];
-      ok = sig_ok(sigs, key_idx, key_valid, nkeys, src(i), r, s);
+      ok = sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s);
       if (ok) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
     }
     fe sv, sm;
@@ -253,10 +254,9 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     const uint64_t i = lane + (uint64_t)j * L;
     const bool ok = (okm >> j) & 1u;
     uint32_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-    const uint64_t si = ok ? src(i) : 0;
     if (ok) {
-      load_be256(sigs + 64 * si, r);
-      load_be256(sigs + 64 * si + 32, s);
+      load_be256(sigs + 64 * i, r);
+      load_be256(sigs + 64 * i + 32, s);
     }
     fe w;
     if (K > 1 && j > 0) {
@@ -274,7 +274,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
       uint32_t u1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, u2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       if (ok) {
         uint32_t e[8];
-        load_be256(hashes + 32 * si, e);
+        load_be256(hashes + 32 * i, e);
         fe ev, rv, t;
         fe_from_words(ev, e);
         fe_from_words(rv, r);
@@ -285,12 +285,14 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
         fn_canon(t, t);
         fe_to_words(u2, t);
       }
-      uint4* o = scal + 4 * i;
-      o[0] = make_uint4(u1[0], u1[1], u1[2], u1[3]);
-      o[1] = make_uint4(u1[4], u1[5], u1[6], u1[7]);
-      o[2] = make_uint4(u2[0], u2[1], u2[2], u2[3]);
-      o[3] = make_uint4(u2[4], u2[5], u2[6], u2[7]);
-      flag[i] = ok ? 1 : 0;
+      SigRec* o = rec + (pos != nullptr ? (uint64_t)pos[i] : i);
+      o->q[0] = make_uint4(u1[0], u1[1], u1[2], u1[3]);
+      o->q[1] = make_uint4(u1[4], u1[5], u1[6], u1[7]);
+      o->q[2] = make_uint4(u2[0], u2[1], u2[2], u2[3]);
+      o->q[3] = make_uint4(u2[4], u2[5], u2[6], u2[7]);
+      o->q[4] = make_uint4(r[0], r[1], r[2], r[3]);
+      o->q[5] = make_uint4(r[4], r[5], r[6], r[7]);
+      o->q[6] = make_uint4(ok ? key_idx[i] : 0u, (uint32_t)i, ok ? 1u : 0u, 0u);
     }
   }
 }
@@ -348,7 +350,7 @@ __global__ void __launch_bounds__(1024) k_key_scan(uint32_t* __restrict__ total,
 }
 
 __global__ void __launch_bounds__(256) k_key_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
-                                                     uint32_t* __restrict__ start, uint32_t* __restrict__ perm) {
+                                                     uint32_t* __restrict__ start, uint32_t* __restrict__ pos) {
   __shared__ uint32_t h[kSortMaxKeys + 1];
   block_key_hist(h, key_idx, n, nkeys);
   for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
@@ -358,7 +360,7 @@ __global__ void __launch_bounds__(256) k_key_scatter(const uint32_t* __restrict_
   const uint64_t hi = lo + chunk < n ? lo + chunk : n;
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     const uint32_t k = key_idx[i];
-    perm[atomicAdd(&h[k < nkeys ? k : nkeys], 1u)] = (uint32_t)i;
+    pos[i] = atomicAdd(&h[k < nkeys ? k : nkeys], 1u);  // signature i's place in key order
   }
 }
 
@@ -391,13 +393,13 @@ size_t key_sort_scratch_bytes(uint64_t n, uint32_t nkeys) { return (size_t)n * 4
 hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (nkeys > kSortMaxKeys) return hipErrorInvalidValue;
-  uint32_t* perm = reinterpret_cast<uint32_t*>(scratch);
-  uint32_t* total = perm + n;
+  uint32_t* pos = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* total = pos + n;
   hipError_t e = hipMemsetAsync(total, 0, (size_t)(nkeys + 1) * 4, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_key_hist, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, total);
   hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(1024), 0, st, total, nkeys + 1);
-  hipLaunchKernelGGL(k_key_scatter, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, total, perm);
+  hipLaunchKernelGGL(k_key_scatter, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, total, pos);
   return hipGetLastError();
 }
 
@@ -457,41 +459,39 @@ size_t scalar_prefix_bytes(uint64_t n) {
 
 template <int K>
 static void launch_scalars_k(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
-                             const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, uint32_t* prefix,
-                             const uint32_t* perm, hipStream_t st) {
+                             const uint32_t* key_valid, uint32_t nkeys, void* rec, uint32_t* prefix,
+                             const uint32_t* pos, hipStream_t st) {
   const uint64_t lanes = (n + K - 1) / K;
   const uint64_t blocks = (lanes + 255) / 256;
   hipLaunchKernelGGL(k_ecdsa_scalars<K>, dim3((uint32_t)blocks), dim3(256), 0, st, hashes, sigs, key_idx, n,
-                     key_valid, nkeys, reinterpret_cast<uint4*>(scal), flag, prefix, perm);
+                     key_valid, nkeys, reinterpret_cast<SigRec*>(rec), prefix, pos);
 }
 
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
-                                const uint32_t* key_valid, uint32_t nkeys, void* scal, uint8_t* flag, void* prefix,
-                                const uint32_t* perm, hipStream_t st) {
+                                const uint32_t* key_valid, uint32_t nkeys, void* rec, void* prefix,
+                                const uint32_t* pos, hipStream_t st) {
   if (n == 0) return hipSuccess;
   uint32_t* pf = reinterpret_cast<uint32_t*>(prefix);
   switch (scalar_batch(n)) {
-    case 1: launch_scalars_k<1>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
-    case 2: launch_scalars_k<2>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
-    case 4: launch_scalars_k<4>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
-    case 8: launch_scalars_k<8>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
-    default: launch_scalars_k<16>(hashes, sigs, key_idx, n, key_valid, nkeys, scal, flag, pf, perm, st); break;
+    case 1: launch_scalars_k<1>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
+    case 2: launch_scalars_k<2>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
+    case 4: launch_scalars_k<4>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
+    case 8: launch_scalars_k<8>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
+    default: launch_scalars_k<16>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_ecdsa_comb(int wg, int wq, const void* scal, const uint8_t* flag, const uint8_t* sigs,
-                             const uint32_t* key_idx, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
-                             uint8_t* bitmap, const uint32_t* perm, uint8_t* okb, hipStream_t st) {
+hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
+                             uint8_t* bitmap, uint8_t* okb, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (perm != nullptr && okb == nullptr) return hipErrorInvalidValue;
-  const CombArgs a{scal, flag, sigs, key_idx, n, gtab, qtabs, bitmap, perm, okb};
+  const CombArgs a{rec, n, gtab, qtabs, bitmap, okb};
   if (launch_comb_part_g29(wg, wq, a, st) || launch_comb_part_g26(wg, wq, a, st) ||
       launch_comb_part_g24(wg, wq, a, st) || launch_comb_part_small(wg, wq, a, st))
     return hipGetLastError();
   return hipErrorInvalidValue;
 }
 
-size_t ecdsa_scratch_bytes(uint64_t n) { return (size_t)n * 64 + (size_t)n; }
+size_t ecdsa_record_bytes(uint64_t n) { return (size_t)n * sizeof(SigRec); }
 
 }  // namespace pbftv

@@ -12,9 +12,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -77,13 +79,14 @@ struct DevBuf {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocCoherent | hipHostMallocMapped;  // plain pinned (DMA staging): hipHostMallocDefault
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 1 << 16);
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocCoherent | hipHostMallocMapped);
+    hipError_t e = hipHostMalloc(&p, want, flags);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -102,6 +105,103 @@ struct HostBuf {
   }
 };
 
+// Persistent host workers for the staging copies of the host-buffer path
+// (one parallel_for at a time; the caller's thread takes part).
+class CopyPool {
+ public:
+  explicit CopyPool(int workers) {
+    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  // fn(part) for part in [0, parts), spread over the workers and the caller
+  template <class F>
+  void parallel_for(int parts, F fn) {
+    std::lock_guard<std::mutex> one(run_mu_);
+    std::function<void(int)> f = fn;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      parts_ = parts;
+      next_ = 0;
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_ == parts_; });
+    job_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      int k;
+      std::function<void(int)>* f;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!job_ || next_ >= parts_) return;
+        k = next_++;
+        f = job_;
+      }
+      (*f)(k);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (++done_ == parts_) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_ != nullptr); });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(int)>* job_ = nullptr;
+  int parts_ = 0, next_ = 0, done_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// parallel memcpy of one large block (pageable caller memory -> pinned staging)
+void par_copy(CopyPool* pool, void* dst, const void* src, size_t bytes) {
+  constexpr size_t kPiece = 1 << 20;
+  if (!pool || bytes < 2 * kPiece) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const int parts = (int)std::min<size_t>((bytes + kPiece - 1) / kPiece, 4 * (size_t)pool->size());
+  const size_t per = (bytes + parts - 1) / parts;
+  pool->parallel_for(parts, [&](int k) {
+    const size_t lo = per * k, hi = std::min(bytes, lo + per);
+    if (hi > lo) std::memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo);
+  });
+}
+
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
@@ -112,16 +212,22 @@ struct Device {
   uint32_t nkeys = 0;
   bool have_keys = false;
   // ecdsa scratch
-  DevBuf hashes, sigs, key_idx, scal, flag, prefix, bitmap;
+  DevBuf hashes, sigs, key_idx, rec, prefix, bitmap;
   DevBuf ksort, okb;  // key order of the lane path (perm + counts) and its per-signature results
   HostBuf stage;  // zero-copy inputs/outputs of the small-batch path
+  // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
+  // path): two slots of pinned staging + device inputs, a copy stream
+  hipStream_t cstream = nullptr;
+  HostBuf pin[2];
+  DevBuf din[2];
+  hipEvent_t h2d_ev[2] = {nullptr, nullptr}, comp_ev[2] = {nullptr, nullptr};
   // sha scratch
   DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
   // message batches (Go-JSON on the device): packed column inputs, verifyMsg bytes,
   // pinned staging for the one H2D and the results
   DevBuf arena, msgok;
   HostBuf mstage, mout;
-  // Device scratch (scal, flag, prefix, ksort, okb, order_scratch) is shared by
+  // Device scratch (rec, prefix, ksort, okb, order_scratch) is shared by
   // calls on d.stream and on caller streams (the *_dev entry points).  The
   // mutex orders the enqueues; this event orders the execution: a call on a
   // different stream than the last scratch user first waits for it.
@@ -189,11 +295,22 @@ hipError_t collect_times(Device& d) {
 struct pbftv_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   bool timing = false;
+  std::unique_ptr<CopyPool> pool;  // staging copies of the host-buffer pipeline
 };
 
 namespace {
 
 constexpr uint64_t kShardAlign = 512;
+
+// staging-copy workers: PBFTV_COPY_THREADS, default min(8, host threads - 1)
+void ensure_pool(pbftv_ctx* ctx) {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  if (ctx->pool) return;
+  int w = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()) - 1);
+  if (const char* e = getenv("PBFTV_COPY_THREADS")) w = std::max(0, atoi(e) - 1);
+  ctx->pool = std::make_unique<CopyPool>(w);
+}
 
 struct Shard {
   uint64_t lo, hi;
@@ -386,12 +503,22 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
-    for (DevBuf* b : {&d->gtab, &d->qtabs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->scal, &d->flag,
+    for (DevBuf* b : {&d->gtab, &d->qtabs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->rec,
                       &d->prefix, &d->bitmap, &d->ksort, &d->okb, &d->data, &d->offsets, &d->lengths, &d->order,
                       &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok})
       b->release();  // explicit, with this device current (the destructors are a backstop)
     for (HostBuf* b : {&d->stage, &d->mstage, &d->mout}) b->release();
     if (d->scratch_ev) (void)hipEventDestroy(d->scratch_ev);
+    for (int k = 0; k < 2; ++k) {
+      d->pin[k].release();
+      d->din[k].release();
+      if (d->h2d_ev[k]) (void)hipEventDestroy(d->h2d_ev[k]);
+      if (d->comp_ev[k]) (void)hipEventDestroy(d->comp_ev[k]);
+    }
+    if (d->cstream) {
+      (void)hipStreamSynchronize(d->cstream);
+      (void)hipStreamDestroy(d->cstream);
+    }
     (void)hipStreamDestroy(d->stream);
   }
   delete ctx;
@@ -410,8 +537,7 @@ int pbftv_reserve(pbftv_ctx* ctx, uint64_t n) {
     Device& d = *dp;
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    HIP_TRY(d.scal.ensure(n * 64));
-    HIP_TRY(d.flag.ensure(n));
+    HIP_TRY(d.rec.ensure(pbftv::ecdsa_record_bytes(n)));
     HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
     if (pbftv::key_sort_wanted(n, d.nkeys)) {
       HIP_TRY(d.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
@@ -432,6 +558,19 @@ int pbftv_dev_alloc(pbftv_ctx* ctx, int dev, uint64_t bytes, void** out_ptr) {
   if (!d || !out_ptr) return fail(PBFTV_EINVAL, "bad context, device index or out pointer");
   HIP_TRY(hipSetDevice(d->id));
   HIP_TRY(hipMalloc(out_ptr, bytes ? bytes : 1));
+  return PBFTV_OK;
+}
+
+int pbftv_host_alloc(pbftv_ctx* ctx, uint64_t bytes, void** out_ptr) {
+  if (!ctx || !out_ptr || ctx->devs.empty()) return fail(PBFTV_EINVAL, "bad context or out pointer");
+  HIP_TRY(hipSetDevice(ctx->devs[0]->id));
+  HIP_TRY(hipHostMalloc(out_ptr, bytes ? bytes : 1, hipHostMallocPortable));
+  return PBFTV_OK;
+}
+
+int pbftv_host_free(pbftv_ctx* ctx, void* ptr) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (ptr) HIP_TRY(hipHostFree(ptr));
   return PBFTV_OK;
 }
 
@@ -473,6 +612,33 @@ int pbftv_memset_dev(pbftv_ctx* ctx, int dev, void* dst, int value, uint64_t byt
 void* pbftv_stream(pbftv_ctx* ctx, int dev) {
   Device* d = dev_of(ctx, dev);
   return d ? reinterpret_cast<void*>(d->stream) : nullptr;
+}
+
+int pbftv_stream_create(pbftv_ctx* ctx, int dev, void** out_stream) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || !out_stream) return fail(PBFTV_EINVAL, "bad context, device index or out pointer");
+  HIP_TRY(hipSetDevice(d->id));
+  hipStream_t st;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  *out_stream = reinterpret_cast<void*>(st);
+  return PBFTV_OK;
+}
+
+int pbftv_stream_destroy(pbftv_ctx* ctx, int dev, void* stream) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || !stream) return fail(PBFTV_EINVAL, "bad context, device index or stream");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  HIP_TRY(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+  return PBFTV_OK;
+}
+
+int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || !stream) return fail(PBFTV_EINVAL, "bad context, device index or stream");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  return PBFTV_OK;
 }
 
 int pbftv_stream_sync(pbftv_ctx* ctx, int dev) {
@@ -676,8 +842,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
     }));
     return PBFTV_OK;
   }
-  HIP_TRY(d.scal.ensure(n * 64));
-  HIP_TRY(d.flag.ensure(n));
+  HIP_TRY(d.rec.ensure(pbftv::ecdsa_record_bytes(n)));
   HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
   HIP_TRY(scratch_acquire(d, st));
   const bool sorted = pbftv::key_sort_wanted(n, d.nkeys);
@@ -686,18 +851,75 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
     HIP_TRY(d.okb.ensure(n));
     HIP_TRY(pbftv::launch_key_sort(d_key_idx, n, d.nkeys, d.ksort.p, st));
   }
-  const uint32_t* perm = sorted ? d.ksort.as<uint32_t>() : nullptr;
+  const uint32_t* pos = sorted ? d.ksort.as<uint32_t>() : nullptr;
   HIP_TRY(timed(d, PBFTV_K_ECDSA_SCALARS, st, [&] {
-    return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, d.scal.p,
-                                       d.flag.as<uint8_t>(), d.prefix.p, perm, st);
+    return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, d.rec.p,
+                                       d.prefix.p, pos, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
-    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.scal.p, d.flag.as<uint8_t>(), d_sigs, d_key_idx, n,
-                                    d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(), d_bitmap, perm,
-                                    sorted ? d.okb.as<uint8_t>() : nullptr, st);
+    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.rec.p, n, d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(),
+                                    d_bitmap, sorted ? d.okb.as<uint8_t>() : nullptr, st);
   }));
   if (sorted) HIP_TRY(pbftv::launch_pack_bits(d.okb.as<uint8_t>(), n, d_bitmap, st));
   HIP_TRY(scratch_release(d, st));
+  return PBFTV_OK;
+}
+
+// Host-buffer verify of one shard, pipelined in chunks over two slots: while
+// chunk k runs on d.stream, chunk k+1 is staged (parallel memcpy into pinned
+// memory, skipped when the caller's buffers are pinned) and DMA'd on
+// d.cstream.  The bitmap comes back in one copy at the end.  Chunk sizes are
+// multiples of 512 (bitmap bytes and waves stay aligned).
+static uint64_t host_chunk(uint64_t m) {
+  uint64_t c = 262144;
+  if (const char* e = getenv("PBFTV_HOST_CHUNK")) c = std::max<uint64_t>(512, strtoull(e, nullptr, 10));
+  c = (c + 511) / 512 * 512;
+  return std::min(c, (m + 511) / 512 * 512);
+}
+
+static int verify_host_pipelined(Device& d, CopyPool* pool, const uint8_t* H, const uint8_t* S, const uint32_t* K,
+                                 uint64_t m, uint8_t* out_bm) {
+  const uint64_t c = host_chunk(m), nch = (m + c - 1) / c;
+  const size_t oh = 0, os = 32 * c, ok = 96 * c, slot = 100 * c;  // slot layout: hashes | sigs | keys
+  if (!d.cstream) HIP_TRY(hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k) {
+    if (!d.h2d_ev[k]) HIP_TRY(hipEventCreateWithFlags(&d.h2d_ev[k], hipEventDisableTiming));
+    if (!d.comp_ev[k]) HIP_TRY(hipEventCreateWithFlags(&d.comp_ev[k], hipEventDisableTiming));
+    HIP_TRY(d.din[k].ensure(slot + 64));
+    if (pool) {
+      d.pin[k].flags = hipHostMallocDefault;
+      HIP_TRY(d.pin[k].ensure(slot + 64));
+    }
+  }
+  HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
+  bool used[2] = {false, false};
+  for (uint64_t j = 0; j < nch; ++j) {
+    const int k = (int)(j & 1);
+    const uint64_t lo = j * c, cnt = std::min(c, m - lo);
+    uint8_t* dv = d.din[k].as<uint8_t>();
+    if (used[k]) HIP_TRY(hipStreamWaitEvent(d.cstream, d.comp_ev[k], 0));  // slot's previous chunk verified
+    if (pool) {
+      if (used[k]) HIP_TRY(hipEventSynchronize(d.h2d_ev[k]));            // its staging copy DMA'd
+      uint8_t* pv = d.pin[k].as<uint8_t>();
+      par_copy(pool, pv + oh, H + 32 * lo, 32 * cnt);
+      par_copy(pool, pv + os, S + 64 * lo, 64 * cnt);
+      par_copy(pool, pv + ok, K + lo, 4 * cnt);
+      HIP_TRY(hipMemcpyAsync(dv, pv, ok + 4 * cnt, hipMemcpyHostToDevice, d.cstream));
+    } else {
+      HIP_TRY(hipMemcpyAsync(dv + oh, H + 32 * lo, 32 * cnt, hipMemcpyHostToDevice, d.cstream));
+      HIP_TRY(hipMemcpyAsync(dv + os, S + 64 * lo, 64 * cnt, hipMemcpyHostToDevice, d.cstream));
+      HIP_TRY(hipMemcpyAsync(dv + ok, K + lo, 4 * cnt, hipMemcpyHostToDevice, d.cstream));
+    }
+    HIP_TRY(hipEventRecord(d.h2d_ev[k], d.cstream));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.h2d_ev[k], 0));
+    int rc = verify_on_device(d, dv + oh, dv + os, reinterpret_cast<const uint32_t*>(dv + ok), cnt,
+                              d.bitmap.as<uint8_t>() + lo / 8, d.stream);
+    if (rc != PBFTV_OK) return rc;
+    HIP_TRY(hipEventRecord(d.comp_ev[k], d.stream));
+    used[k] = true;
+  }
+  HIP_TRY(hipMemcpyAsync(out_bm, d.bitmap.p, (m + 7) / 8, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
   return PBFTV_OK;
 }
 
@@ -758,23 +980,13 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((res[i] & 1u) << (i & 7));
     return PBFTV_OK;
   }
+  const bool pinned = is_pinned(hashes) && is_pinned(sig_rs) && is_pinned(key_idx);
+  if (!pinned) ensure_pool(ctx);
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
-    const uint64_t m = s.hi - s.lo;
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    HIP_TRY(d.hashes.ensure(m * 32));
-    HIP_TRY(d.sigs.ensure(m * 64));
-    HIP_TRY(d.key_idx.ensure(m * 4));
-    HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
-    HIP_TRY(hipMemcpyAsync(d.hashes.p, hashes + 32 * s.lo, m * 32, hipMemcpyHostToDevice, d.stream));
-    HIP_TRY(hipMemcpyAsync(d.sigs.p, sig_rs + 64 * s.lo, m * 64, hipMemcpyHostToDevice, d.stream));
-    HIP_TRY(hipMemcpyAsync(d.key_idx.p, key_idx + s.lo, m * 4, hipMemcpyHostToDevice, d.stream));
-    int rc = verify_on_device(d, d.hashes.as<uint8_t>(), d.sigs.as<uint8_t>(), d.key_idx.as<uint32_t>(), m,
-                              d.bitmap.as<uint8_t>(), d.stream);
-    if (rc != PBFTV_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(out_bitmap + s.lo / 8, d.bitmap.p, (m + 7) / 8, hipMemcpyDeviceToHost, d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));
-    return PBFTV_OK;
+    return verify_host_pipelined(d, pinned ? nullptr : ctx->pool.get(), hashes + 32 * s.lo, sig_rs + 64 * s.lo,
+                                 key_idx + s.lo, s.hi - s.lo, out_bitmap + s.lo / 8);
   });
 }
 

@@ -32,6 +32,13 @@ __device__ __forceinline__ void load_be256(const uint8_t* __restrict__ p, uint32
   w[3] = bswap32(b.x); w[2] = bswap32(b.y); w[1] = bswap32(b.z); w[0] = bswap32(b.w);
 }
 
+// Stage 1 -> stage 2 handoff, one per signature at its position in key order:
+// q[0..1] u1, q[2..3] u2, q[4..5] r (LE words), q[6] = {key index, batch
+// index, ok, 0}, q[7] unused (a full 128-B line per record).
+struct alignas(128) SigRec {
+  uint4 q[8];
+};
+
 __device__ __forceinline__ bool sig_ok(const uint8_t* __restrict__ sigs, const uint32_t* __restrict__ key_idx,
                                        const uint32_t* __restrict__ key_valid, uint32_t nkeys, uint64_t i,
                                        uint32_t r[8], uint32_t s[8]) {
@@ -124,15 +131,14 @@ __device__ bool comb2_dev_pass(Acc& acc, const uint32_t u1[8], const uint32_t u2
 // stays in registers (a jac passed by reference would live in scratch and
 // cost a 108-byte store + load per addition).
 template <int WG, int WQ>
-__device__ __noinline__ bool comb2_checked_verify(const uint4* __restrict__ sp, const uint8_t* __restrict__ sig,
-                                                  const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
-  const uint4 a = sp[0], b = sp[1], c = sp[2], dd = sp[3];
+__device__ __noinline__ bool comb2_checked_verify(const SigRec* __restrict__ rp, const uint4* __restrict__ gtab,
+                                                  const uint4* __restrict__ qtab) {
+  const uint4 a = rp->q[0], b = rp->q[1], c = rp->q[2], dd = rp->q[3], e = rp->q[4], f = rp->q[5];
   const uint32_t u1[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   const uint32_t u2[8] = {c.x, c.y, c.z, c.w, dd.x, dd.y, dd.z, dd.w};
+  const uint32_t r[8] = {e.x, e.y, e.z, e.w, f.x, f.y, f.z, f.w};
   jac R;
   const bool fin = comb2_dev_pass<true, WG, WQ>(R, u1, u2, gtab, qtab);
-  uint32_t r[8];
-  load_be256(sig, r);
   return ecdsa_check(R, fin, r);
 }
 
@@ -183,14 +189,11 @@ __device__ __forceinline__ void read_entry_lds(uint4 (*sent)[256], uint32_t t, u
 }
 
 template <int WG, int WQ>
-__global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint4* __restrict__ scal, const uint8_t* __restrict__ flag,
-                                                       const uint8_t* __restrict__ sigs,
-                                                       const uint32_t* __restrict__ key_idx, uint64_t n,
-                                                       const uint4* __restrict__ gtab,
-                                                       const uint4* __restrict__ qtabs,
-                                                       uint8_t* __restrict__ bitmap,
-                                                       const uint32_t* __restrict__ perm,
-                                                       uint8_t* __restrict__ okb) {
+__global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigRec* __restrict__ rec, uint64_t n,
+                                                                    const uint4* __restrict__ gtab,
+                                                                    const uint4* __restrict__ qtabs,
+                                                                    uint8_t* __restrict__ bitmap,
+                                                                    uint8_t* __restrict__ okb) {
   using S = CombSteps<WG, WQ>;
   // signed digits of u1 / u2 in step order, one column per thread: recoded once
   // in the prologue so the main loop holds no 256-bit digit shift registers
@@ -199,15 +202,16 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint
   // while it is in flight): piece k of thread t at sent[k][t]
   __shared__ uint4 sent[4][256];
   const uint32_t t = threadIdx.x;
-  // lane position p; with a key order (k_key_*), p is the p-th signature by key
+  // lane p reads record p: with a key order (k_key_*) the p-th signature by key,
+  // written there by stage 1 (coalesced: no gather through a permutation)
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + t;
-  const uint64_t i = perm != nullptr && p < n ? (uint64_t)perm[p] : p;
-  const bool active = p < n && flag[p];  // stage 1 wrote scal/flag in the same (key) order
+  const SigRec* rp = rec + p;
+  uint4 meta = make_uint4(0, 0, 0, 0);  // key, batch index, ok
+  if (p < n) meta = rp->q[6];
   bool ok = false;
-  if (active) {
-    const uint4* sp = scal + 4 * p;
+  if (meta.z != 0) {
     {
-      const uint4 a = sp[0], b = sp[1], c = sp[2], dd = sp[3];
+      const uint4 a = rp->q[0], b = rp->q[1], c = rp->q[2], dd = rp->q[3];
       digit_stream<WG> s1;
       digit_stream<WQ> s2;
       s1.w[0] = a.x; s1.w[1] = a.y; s1.w[2] = a.z; s1.w[3] = a.w;
@@ -218,7 +222,7 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint
       PBFTV_UNROLL for (int j = 0; j < S::nD; ++j)
         sdig[j][t] = (typename S::Digit)((S::is_q(j) ? s2.next() : s1.next()) - 1);
     }
-    const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
+    const uint4* qtab = qtabs + (uint64_t)meta.x * (CombGeom<WQ>::kWords / 4);
     xyzz_s R;  // signed-limb accumulator (fes.h)
     bool inf = true;
     int d = (int)sdig[0][t] + 1;
@@ -249,18 +253,18 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const uint
       }
     }
     if (!inf && fs_is_zero(R.zz)) {
-      ok = comb2_checked_verify<WG, WQ>(sp, sigs + 64 * i, gtab, qtab);  // exceptional step: redo
+      ok = comb2_checked_verify<WG, WQ>(rp, gtab, qtab);  // exceptional step: redo
     } else {
-      uint32_t r[8];
-      load_be256(sigs + 64 * i, r);
+      const uint4 e = rp->q[4], f = rp->q[5];
+      const uint32_t r[8] = {e.x, e.y, e.z, e.w, f.x, f.y, f.z, f.w};
       ok = ecdsa_check(R, !inf, r);
     }
   }
-  if (perm != nullptr) {  // key order: one byte per signature, k_pack_bits builds the bitmap
-    if (p < n) okb[i] = ok ? 1 : 0;
+  if (okb != nullptr) {  // key order: one byte at the signature's own index, k_pack_bits builds the bitmap
+    if (p < n) okb[meta.y] = ok ? 1 : 0;
     return;
   }
-  // LSB-first bitmap: wave ballot, lanes 0..7 store one byte each
+  // arrival order: LSB-first bitmap by wave ballot, lanes 0..7 store one byte each
   const unsigned long long m = __ballot(ok);
   const uint32_t lane = t & 63u;
   const uint64_t wave_base = p - lane;
@@ -388,48 +392,49 @@ __device__ __forceinline__ void quad_mul(fe& p, int role, const fe& a0, const fe
   fe a, b;
   quad_sel(a, role, a0, a1, a2, a3);
   quad_sel(b, role, b0, b1, b2, b3);
-  fe_mul(p, a, b);
+  fs_mul(p, a, b);  // signed-limb product (fes.h): operands S- or D-type
 }
 
-// (gx, gy) + (qx, qy), both affine, into XYZZ (mmadd-2008-s, 3 steps); exc if
-// the x-coordinates meet.
-__device__ __forceinline__ void quad_mmadd_xyzz(xyzz& r, bool& exc, int role, const fe& gx, const fe& gy,
+// (gx, gy) + (qx, qy), both affine S-type, into XYZZ (mmadd-2008-s, 3 steps);
+// exc if the x-coordinates meet.  Signed-limb arithmetic (fes.h): differences
+// are D-type, X3 is renormalised (S), Y3 stays D-type (only multiplied later).
+__device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, bool& exc, int role, const fe& gx, const fe& gy,
                                                 const fe& qx, const fe& qy) {
   fe p, rr, pp, r2, ppp, qq, x3, t, a, b, prod;
-  fe_sub(p, qx, gx);
-  fe_sub(rr, qy, gy);
-  exc = fe_is_zero(p);
+  fs_sub(p, qx, gx);
+  fs_sub(rr, qy, gy);
+  exc = fs_is_zero(p);
   quad_mul(prod, role, p, p, rr, rr, p, p, rr, rr);          // PP, R^2
   quad_bcast<0>(pp, prod);
   quad_bcast<1>(r2, prod);
   quad_mul(prod, role, p, pp, gx, pp, p, pp, gx, pp);        // PPP, Q = X1 PP
   quad_bcast<0>(ppp, prod);
   quad_bcast<1>(qq, prod);
-  fe_add(t, ppp, qq);
-  fe_add(t, t, qq);
-  fe_sub(x3, r2, t);                                         // X3 = R^2 - PPP - 2Q
-  fe_sub(t, qq, x3);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) x3.v[i] = r2.v[i] - ppp.v[i] - (qq.v[i] << 1);
+  fs_norm(x3, x3);                                           // X3 = R^2 - PPP - 2Q
+  fs_sub(t, qq, x3);
   quad_mul(prod, role, rr, t, gy, ppp, rr, t, gy, ppp);      // R (Q - X3), Y1 PPP
   quad_bcast<0>(a, prod);
   quad_bcast<1>(b, prod);
-  fe_sub(r.y, a, b);
+  fs_sub(r.y, a, b);
   r.x = x3;
   r.zz = pp;
   r.zzz = ppp;
 }
 
-// r = P + Q (both finite XYZZ), add-2008-s in 4 steps of <= 4 products (the
-// Jacobian quad_jadd needs 5); exc if the x-coordinates meet (P == 0).
-__device__ __forceinline__ void quad_xyzz_add(xyzz& r, bool& exc, int role, const xyzz& P, const xyzz& Q) {
+// r = P + Q (both finite XYZZ: X, ZZ, ZZZ S-type, Y S- or D-type), add-2008-s
+// in 4 steps of <= 4 products (the Jacobian quad_jadd needs 5); exc if the
+// x-coordinates meet (P == 0).
+__device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, bool& exc, int role, const xyzz_s& P, const xyzz_s& Q) {
   fe prod, u1, u2, s1, s2, p, rr, pp, r2, zz12, zzz12, ppp, qq, x3, t, a, b;
   quad_mul(prod, role, P.x, Q.zz, Q.x, P.zz, P.y, Q.zzz, Q.y, P.zzz);      // U1, U2, S1, S2
   quad_bcast<0>(u1, prod);
   quad_bcast<1>(u2, prod);
   quad_bcast<2>(s1, prod);
   quad_bcast<3>(s2, prod);
-  fe_sub(p, u2, u1);
-  fe_sub(rr, s2, s1);
-  exc = fe_is_zero(p);
+  fs_sub(p, u2, u1);
+  fs_sub(rr, s2, s1);
+  exc = fs_is_zero(p);
   quad_mul(prod, role, p, p, rr, rr, P.zz, Q.zz, P.zzz, Q.zzz);             // PP, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2
   quad_bcast<0>(pp, prod);
   quad_bcast<1>(r2, prod);
@@ -439,15 +444,14 @@ __device__ __forceinline__ void quad_xyzz_add(xyzz& r, bool& exc, int role, cons
   quad_bcast<0>(ppp, prod);
   quad_bcast<1>(qq, prod);
   quad_bcast<2>(r.zz, prod);
-  fe_add(t, ppp, qq);
-  fe_add(t, t, qq);
-  fe_sub(x3, r2, t);                                                        // X3 = R^2 - PPP - 2Q
-  fe_sub(t, qq, x3);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) x3.v[i] = r2.v[i] - ppp.v[i] - (qq.v[i] << 1);
+  fs_norm(x3, x3);                                                          // X3 = R^2 - PPP - 2Q
+  fs_sub(t, qq, x3);
   quad_mul(prod, role, rr, t, s1, ppp, zzz12, ppp, zzz12, ppp);             // R (Q - X3), S1 PPP, ZZZ3
   quad_bcast<0>(a, prod);
   quad_bcast<1>(b, prod);
   quad_bcast<2>(r.zzz, prod);
-  fe_sub(r.y, a, b);                                                        // Y3 = R (Q - X3) - S1 PPP
+  fs_sub(r.y, a, b);                                                        // Y3 = R (Q - X3) - S1 PPP
   r.x = x3;
 }
 
@@ -455,7 +459,7 @@ __device__ __forceinline__ void quad_xyzz_add(xyzz& r, bool& exc, int role, cons
 // exc reports a doubling / cancellation anywhere (the caller reruns the
 // signature with wave_sum_lanes).
 template <int WG, int WQ>
-__device__ __forceinline__ void wave_sum_quads(xyzz& P, bool& inf, bool& exc, const uint32_t u1[8],
+__device__ __forceinline__ void wave_sum_quads(xyzz_s& P, bool& inf, bool& exc, const uint32_t u1[8],
                                                const uint32_t u2[8], const uint4* __restrict__ gtab,
                                                const uint4* __restrict__ qtab) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
@@ -475,20 +479,16 @@ __device__ __forceinline__ void wave_sum_quads(xyzz& P, bool& inf, bool& exc, co
   uint32_t w16[16];
   load_entry<WG>(gtab, q < nG ? q : 0, d1, eg);
   load_entry<WQ>(qtab, q < nQ ? q : 0, d2, eq);
-  fe gx, gy, qx, qy, ny;
+  fe gx, gy, qx, qy;
   entry_words(eg, w16);
   entry_to_fe(gx, gy, w16);
-  if (d1 < 0) {
-    fe_neg_lazy(ny, gy);
-    fe_norm(gy, ny);
-  }
+  fs_cneg(gy, gy, d1 < 0);
+  fs_norm(gy, gy);  // S-type: R = qy - gy must stay D-type
   entry_words(eq, w16);
   entry_to_fe(qx, qy, w16);
-  if (d2 < 0) {
-    fe_neg_lazy(ny, qy);
-    fe_norm(qy, ny);
-  }
-  xyzz S;
+  fs_cneg(qy, qy, d2 < 0);
+  fs_norm(qy, qy);
+  xyzz_s S;
   bool e0;
   quad_mmadd_xyzz(S, e0, role, gx, gy, qx, qy);       // every quad runs it; selected below
   exc = d1 != 0 && d2 != 0 && e0;
@@ -502,7 +502,7 @@ __device__ __forceinline__ void wave_sum_quads(xyzz& P, bool& inf, bool& exc, co
   fe_sel3(P.zzz, both, S.zzz, true, one, one);
 #pragma unroll 1
   for (int m = 1; m < nW; m <<= 1) {
-    xyzz Q;
+    xyzz_s Q;
     shfl_xor_fe(Q.x, P.x, 4 * m);
     shfl_xor_fe(Q.y, P.y, 4 * m);
     shfl_xor_fe(Q.zz, P.zz, 4 * m);
@@ -562,7 +562,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
     bool inf;
     bool exc = true;
     if constexpr (nW <= 16) {
-      xyzz P;
+      xyzz_s P;
       wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
       exc = __any(exc);
       if (!exc) ok = ecdsa_check(P, !inf, r);
@@ -598,13 +598,12 @@ void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* k
 }
 
 template <int WG, int WQ>
-void launch_comb_w(const void* scal, const uint8_t* flag, const uint8_t* sigs, const uint32_t* key_idx,
-                          uint64_t n, const uint32_t* gtab, const uint32_t* qtabs, uint8_t* bitmap,
-                          const uint32_t* perm, uint8_t* okb, hipStream_t st) {
+void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs, uint8_t* bitmap,
+                   uint8_t* okb, hipStream_t st) {
   const uint64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL((k_ecdsa_comb<WG, WQ>), dim3((uint32_t)blocks), dim3(256), 0, st,
-                     reinterpret_cast<const uint4*>(scal), flag, sigs, key_idx, n,
-                     reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4*>(qtabs), bitmap, perm, okb);
+                     reinterpret_cast<const SigRec*>(rec), n, reinterpret_cast<const uint4*>(gtab),
+                     reinterpret_cast<const uint4*>(qtabs), bitmap, okb);
 }
 
 // One instantiation unit: the dispatchers for the geometry pairs COMBOS(X).
@@ -619,7 +618,7 @@ void launch_comb_w(const void* scal, const uint8_t* flag, const uint8_t* sigs, c
   }
 #define PBFTV_PART_COMB_CASE(G, Q)                                                                            \
   if (wg == G && wq == Q) {                                                                                   \
-    launch_comb_w<G, Q>(a.scal, a.flag, a.sigs, a.key_idx, a.n, a.gtab, a.qtabs, a.bitmap, a.perm, a.okb, st); \
+    launch_comb_w<G, Q>(a.rec, a.n, a.gtab, a.qtabs, a.bitmap, a.okb, st);                                    \
     return true;                                                                                              \
   }
 #define PBFTV_PART_WAVE_CASE(G, Q)                                                                            \

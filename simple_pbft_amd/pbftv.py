@@ -58,11 +58,16 @@ def lib() -> ctypes.CDLL:
         "pbftv_reserve": (ctypes.c_int, [_vp, ctypes.c_uint64]),
         "pbftv_dev_alloc": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(_vp)]),
         "pbftv_dev_free": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+        "pbftv_host_alloc": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),
+        "pbftv_host_free": (ctypes.c_int, [_vp, _vp]),
         "pbftv_memcpy_h2d": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_uint64]),
         "pbftv_memcpy_d2h": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_uint64]),
         "pbftv_memset_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint64]),
         "pbftv_stream": (_vp, [_vp, ctypes.c_int]),
         "pbftv_stream_sync": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "pbftv_stream_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(_vp)]),
+        "pbftv_stream_destroy": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+        "pbftv_stream_wait": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
         "pbftv_set_kernel_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
         "pbftv_kernel_time_ms": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_uint64)]),
@@ -326,6 +331,26 @@ class DeviceBuffer:
         self.ptr = 0
 
 
+class PinnedArray:
+    """A numpy view of pbftv_host_alloc memory (pinned: host-buffer verifies
+    from it skip the staging copy).  Free with .free() before the Verifier closes."""
+
+    def __init__(self, ver: "Verifier", shape, dtype):
+        self.ver = ver
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        p = ctypes.c_void_p()
+        _check(ver._L.pbftv_host_alloc(ver._h, max(nbytes, 1), ctypes.byref(p)))
+        self.ptr = p.value
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(self.ptr)
+        self.a = np.frombuffer(buf, np.uint8)[:nbytes].view(dtype).reshape(shape)
+
+    def free(self):
+        if self.ptr and self.ver._h is not None:
+            self.a = None
+            _check(self.ver._L.pbftv_host_free(self.ver._h, self.ptr))
+        self.ptr = 0
+
+
 class Verifier:
     """A pbftv_ctx: the GPUs in device_mask (0 = all visible gfx950 devices)."""
 
@@ -380,8 +405,26 @@ class Verifier:
             _check(self._L.pbftv_memset_dev(self._h, dev, buf.ptr + arr.nbytes, 0, pad))
         return buf
 
+    def pinned(self, arr: np.ndarray) -> PinnedArray:
+        """A pinned copy of arr (pbftv_host_alloc)."""
+        arr = np.ascontiguousarray(arr)
+        p = PinnedArray(self, arr.shape, arr.dtype)
+        p.a[...] = arr
+        return p
+
     def stream(self, dev: int) -> int:
         return self._L.pbftv_stream(self._h, dev)
+
+    def stream_create(self, dev: int) -> int:
+        st = ctypes.c_void_p()
+        _check(self._L.pbftv_stream_create(self._h, dev, ctypes.byref(st)))
+        return st.value
+
+    def stream_destroy(self, dev: int, stream: int):
+        _check(self._L.pbftv_stream_destroy(self._h, dev, stream))
+
+    def stream_wait(self, dev: int, stream: int):
+        _check(self._L.pbftv_stream_wait(self._h, dev, stream))
 
     def sync(self, dev: int):
         _check(self._L.pbftv_stream_sync(self._h, dev))

@@ -322,3 +322,71 @@ def test_ecdsa_wave_path_edge_counts(ver, oracle_lib, monkeypatch):
     for n in (1, 2, 7, 8, 9, 15, 16, 17, 67, 2047, 2048, 2049, 2400):
         got = ver.verify_batch(hashes[:n], sigs[:n], kidx[:n])
         assert (got == want[:n]).all(), n
+
+
+# ---- host-buffer pipeline (pbftv_api.cpp verify_host_pipelined) ------------
+@pytest.mark.parametrize("chunk", ["512", "4096", "262144"])
+def test_host_pipeline_chunks_pageable_and_pinned(ver, oracle_lib, chunk, monkeypatch):
+    """The chunked host-buffer path (staging copy -> DMA -> verify, two slots in
+    flight) at chunk sizes that give 1, a few and many chunks, a ragged tail,
+    from pageable numpy memory and from pbftv_host_alloc memory (no staging),
+    against the corruption mask (1 %) and the oracle on a sample."""
+    monkeypatch.setenv("PBFTV_HOST_CHUNK", chunk)
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=16, per_key=32, seed=55)
+    n = 40_000 + 123
+    rng = np.random.default_rng(56)
+    o = rng.integers(0, len(kidx), n)
+    H, S, K = hashes[o].copy(), sigs[o].copy(), kidx[o].copy()
+    bad = rng.random(n) < 0.01
+    S[np.nonzero(bad)[0], 50] ^= 4
+    ver.register_keys(keys)
+    got = ver.verify_batch(H, S, K)
+    assert (got == ~bad).all()
+    pins = [ver.pinned(a) for a in (H, S, K)]
+    try:
+        got2 = ver.verify_batch(*(p.a for p in pins))
+        assert (got2 == got).all()
+    finally:
+        for p in pins:
+            p.free()
+    m = 3000
+    want = np.zeros((m + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(H.ctypes.data, S.ctypes.data, K.ctypes.data, m, keys.ctypes.data,
+                                              len(keys), want.ctypes.data, 8)
+    assert (np.unpackbits(want, bitorder="little")[:m].astype(bool) == got[:m]).all()
+
+
+def test_dev_calls_on_two_streams_share_scratch(ver, oracle_lib, monkeypatch):
+    """*_dev calls on a caller stream and on the context stream reuse
+    the device scratch (scalars, flags, key order); the scratch event orders
+    them.  Two different batches enqueued back to back on two streams must both
+    come out right."""
+    monkeypatch.setenv("PBFTV_WAVE_MAX", "0")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=12, per_key=16, seed=57)
+    ver.register_keys(keys)
+    n = 65536
+    rng = np.random.default_rng(58)
+    bufs, masks = [], []
+    for t in range(2):
+        o = rng.integers(0, len(kidx), n)
+        H, S, K = hashes[o].copy(), sigs[o].copy(), kidx[o].copy()
+        bad = rng.random(n) < (0.02 if t == 0 else 0.3)
+        S[np.nonzero(bad)[0], 20] ^= 1
+        bufs.append((ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K), ver.alloc(0, n // 8)))
+        masks.append(~bad)
+    side = ver.stream_create(0)
+    try:
+        for _ in range(3):
+            (h0, s0, k0, b0), (h1, s1, k1, b1) = bufs
+            ver.verify_batch_dev(0, h0.ptr, s0.ptr, k0.ptr, n, b0.ptr, stream=side)
+            ver.verify_batch_dev(0, h1.ptr, s1.ptr, k1.ptr, n, b1.ptr)
+            ver.sync(0)
+            ver.stream_wait(0, side)
+            for (_, _, _, b), want in zip(bufs, masks):
+                got = np.unpackbits(b.to_host(), bitorder="little")[:n].astype(bool)
+                assert (got == want).all()
+    finally:
+        ver.stream_destroy(0, side)
+        for tup in bufs:
+            for b in tup:
+                b.free()

@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(64) probe(const uint8_t* hashes, const uint8_t
   acc += u1[0] ^ u2[0];
   t[2] = wall_clock64();
   const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
-  xyzz P;
+  xyzz_s P;
   bool inf, exc;
   wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
   acc += P.x.v[0] ^ (uint32_t)exc;
