@@ -263,44 +263,62 @@ def _timed(ver, fn, reps):
 
 
 def run_config1(ver, n_req=1000):
-    """configs[0]: the reference 4-node pattern for 1k requests, end to end from
-    host buffers: digest(request) once per request, then every received vote
-    (9 prepare + 12 commit checks per request) through ONE pool flush
-    (pbftv_flush_votes: Go-JSON preimage + SHA-256 + verifyMsg against its
-    request's State + ECDSA, on the device), and the 4 replies per request
-    (Go-JSON + SHA-256 on the device, then one ECDSA batch).  The messages are
-    laid out column-wise before timing, as a cgo shim would hand over a pool
-    snapshot."""
-    from simple_pbft_amd.pbftv import ReplyColumns, RequestColumns, VoteColumns
-    pub, reqs, votes, vsig, replies, rsig, checks = synth.config1_cluster(n_req)
-    ver.register_keys(pub)
+    """configs[0]: the reference 4-node pattern for 1k requests with every
+    message signed, end to end from host buffers, one device
+    round trip per message kind (Go-JSON preimage + SHA-256 + checks + ECDSA on
+    the device):
+      requests     pbftv_flush_requests: client signature over the request as
+                   sent, plus the StartConsensus digest with the assigned
+                   sequence ID (pbft_impl.go:57-73)
+      pre-prepares pbftv_flush_preprepares: primary's signature + verifyMsg
+                   against each receiving replica's State, 3 receipts/request
+      votes        pbftv_flush_votes: 9 prepare + 12 commit receipts/request,
+                   verifyMsg against the request's State + signature
+      replies      pbftv_flush_replies: 4 per request, the client checks them
+    The messages are laid out column-wise before timing, as a cgo shim would
+    hand over a pool snapshot."""
+    from simple_pbft_amd.pbftv import PrePrepareColumns, ReplyColumns, RequestColumns, VoteColumns
+    c = synth.config1_cluster(n_req)
+    ver.register_keys(c["pub"])
     node_of = {nid: j for j, nid in enumerate(synth.NODES)}
-    vi = np.array([c[1] for c in checks if c[0] == "vote"], np.int64)
-    ri = np.array([c[1] for c in checks if c[0] == "reply"], np.int64)
-    seq_to_r = {reqs[r][3]: r for r in range(n_req)}
-    req_cols = RequestColumns(reqs)
+    checks = c["checks"]
+
+    def idx(kind):
+        return np.array([x[1] for x in checks if x[0] == kind], np.int64)
+    qi, pi, vi, ri = idx("request"), idx("preprepare"), idx("vote"), idx("reply")
+    votes, replies, pps = c["votes"], c["replies"], c["preprepares"]
+    seq_to_r = {int(s): r for r, s in enumerate(c["assigned_seqs"])}
+    req_cols = RequestColumns([c["requests"][j] for j in qi])
+    qS, qK = np.ascontiguousarray(c["request_sigs"][qi]), np.full(len(qi), synth.CLIENT_KEY, np.uint32)
+    aseq = np.ascontiguousarray(c["assigned_seqs"][qi])
+    pp_cols = PrePrepareColumns([pps[j] for j in pi])          # one entry per replica receipt
+    pS, pK = np.ascontiguousarray(c["preprepare_sigs"][pi]), np.zeros(len(pi), np.uint32)
+    p_state = np.array([seq_to_r[pps[j][1]] for j in pi], np.uint32)
     vote_cols = VoteColumns([votes[j] for j in vi])            # one entry per received vote
-    vS = np.ascontiguousarray(vsig[vi])
+    vS = np.ascontiguousarray(c["vote_sigs"][vi])
     vK = np.array([node_of[votes[j][3]] for j in vi], np.uint32)
     v_state = np.array([seq_to_r[votes[j][1]] for j in vi], np.uint32)
     s_view = np.full(n_req, synth.VIEW, np.int64)
     s_last = np.full(n_req, -1, np.int64)
     rep_cols = ReplyColumns([replies[j] for j in ri])
-    rS = np.ascontiguousarray(rsig[ri])
+    rS = np.ascontiguousarray(c["reply_sigs"][ri])
     rK = np.array([node_of[replies[j][3]] for j in ri], np.uint32)
     state = {}
 
     def flow():
-        req_d = ver.digest_request_batch(req_cols)             # digest(request), once per request
-        _, sig_ok, msg_ok = ver.flush_votes(vote_cols, vS, vK, (s_view, s_last, req_d), v_state, digests=False)
-        rep_ok = ver.verify_batch(ver.digest_reply_batch(rep_cols), rS, rK)
-        state["ok"] = bool(sig_ok.all() and msg_ok.all() and rep_ok.all())
+        _, q_ok, req_d = ver.flush_requests(req_cols, qS, qK, aseq, digests=False)
+        _, _, p_ok, pm_ok = ver.flush_preprepares(pp_cols, pS, pK, (s_view, s_last), p_state, digests=False)
+        _, v_ok, vm_ok = ver.flush_votes(vote_cols, vS, vK, (s_view, s_last, req_d), v_state, digests=False)
+        _, r_ok = ver.flush_replies(rep_cols, rS, rK, digests=False)
+        state["ok"] = bool(q_ok.all() and p_ok.all() and pm_ok.all() and v_ok.all() and vm_ok.all() and r_ok.all())
 
     best, med = _timed(ver, flow, 5)
-    n_sig = len(vi) + len(ri)
-    return {"workload": f"config1: 4-node pattern, {n_req} requests, {n_sig} signature checks, "
-                        f"{n_req + n_sig} Go-JSON digests (built on the device), {len(vi)} verifyMsg, "
-                        "end-to-end from host buffers",
+    n_sig = len(qi) + len(pi) + len(vi) + len(ri)
+    n_dig = 2 * len(qi) + 2 * len(pi) + len(vi) + len(ri)
+    return {"workload": f"config1: 4-node pattern, {n_req} requests, every message signed: {n_sig} signature "
+                        f"checks ({len(qi)} requests, {len(pi)} pre-prepares, {len(vi)} votes, {len(ri)} replies), "
+                        f"{n_dig} Go-JSON digests built on the device, {len(pi) + len(vi)} verifyMsg, "
+                        "4 flush calls end-to-end from host buffers",
             "verifies_per_s": n_sig / best, "ms": best * 1e3, "ms_median": med * 1e3, "check": state.get("ok")}
 
 

@@ -144,6 +144,25 @@ uint64_t pbftv_gojson_vote(int64_t view_id, int64_t sequence_id, const char* dig
 uint64_t pbftv_gojson_vote_signed(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
                                   const char* node_id, uint64_t node_id_len, int64_t msg_type, const uint8_t* sig,
                                   uint64_t sig_len, int sig_nil, uint8_t* out, uint64_t cap);
+/* Signed RequestMsg / ReplyMsg / PrePrepareMsg on the wire:
+ * the struct of pbft_msg_types.go:3-23 followed by "signature" as above.  Each
+ * signing preimage is the unsigned encoding (pbftv_gojson_request / _reply /
+ * _preprepare).  A client signs its request with the sequenceID it sent (the
+ * reference's clients leave it 0; StartConsensus assigns it, pbft_impl.go:67);
+ * a pre-prepare's embedded request carries the client's signature on the wire
+ * (req_sig*), while the primary's preimage embeds the unsigned request. */
+uint64_t pbftv_gojson_request_signed(int64_t timestamp, const char* client_id, uint64_t client_id_len,
+                                     const char* operation, uint64_t operation_len, int64_t sequence_id,
+                                     const uint8_t* sig, uint64_t sig_len, int sig_nil, uint8_t* out, uint64_t cap);
+uint64_t pbftv_gojson_reply_signed(int64_t view_id, int64_t timestamp, const char* client_id, uint64_t client_id_len,
+                                   const char* node_id, uint64_t node_id_len, const char* result, uint64_t result_len,
+                                   const uint8_t* sig, uint64_t sig_len, int sig_nil, uint8_t* out, uint64_t cap);
+uint64_t pbftv_gojson_preprepare_signed(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                                        int has_request, int64_t req_timestamp, const char* req_client_id,
+                                        uint64_t req_client_id_len, const char* req_operation,
+                                        uint64_t req_operation_len, int64_t req_sequence_id, const uint8_t* req_sig,
+                                        uint64_t req_sig_len, int req_sig_nil, const uint8_t* sig, uint64_t sig_len,
+                                        int sig_nil, uint8_t* out, uint64_t cap);
 uint64_t pbftv_gojson_reply(int64_t view_id, int64_t timestamp, const char* client_id, uint64_t client_id_len,
                             const char* node_id, uint64_t node_id_len, const char* result, uint64_t result_len,
                             uint8_t* out, uint64_t cap);
@@ -215,6 +234,47 @@ int pbftv_flush_votes(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const
                       const int64_t* state_view_ids, const int64_t* state_last_seqs,
                       const uint8_t* state_req_digests, const uint32_t* state_idx, uint8_t* out_digests,
                       uint8_t* out_sig_bitmap, uint8_t* out_msg_bitmap);
+
+/* Flushes of the other three signed messages, one GPU round
+ * trip per device like pbftv_flush_votes; every output is optional (NULL = not
+ * wanted; a signature bitmap needs sig_rs n*64 BE and key_idx).
+ *
+ * Requests (GetReq / resolveRequestMsg, pbft/network/node.go:150-177, 521-538):
+ *   h_i = SHA-256(Go-JSON(RequestMsg i with sequence_ids[i]))  -> out_digests
+ *   sig bit i = ecdsa.Verify(key[key_idx[i]], h_i, r_i, s_i)  -> out_sig_bitmap
+ *   c_i = digest(RequestMsg i with SequenceID = assigned_seqs[i]), the
+ *         StartConsensus digest (pbft_impl.go:67-73)          -> out_consensus_digests
+ *                                                                (needs assigned_seqs) */
+int pbftv_flush_requests(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
+                         const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
+                         const uint64_t* operation_off, const uint32_t* operation_len, const int64_t* sequence_ids,
+                         const uint8_t* sig_rs, const uint32_t* key_idx, const int64_t* assigned_seqs,
+                         uint8_t* out_digests, uint8_t* out_sig_bitmap, uint8_t* out_consensus_digests);
+/* Replies (the client's reply collection, node.go:182-197 / client):
+ *   h_i = SHA-256(Go-JSON(ReplyMsg i)) -> out_digests; sig bit i as above. */
+int pbftv_flush_replies(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* timestamps,
+                        const uint8_t* client_ids, const uint64_t* client_id_off, const uint32_t* client_id_len,
+                        const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                        const uint8_t* results, const uint64_t* result_off, const uint32_t* result_len,
+                        const uint8_t* sig_rs, const uint32_t* key_idx, uint8_t* out_digests,
+                        uint8_t* out_sig_bitmap);
+/* Pre-prepares (replicas, State.PrePrepare pbft_impl.go:91-109):
+ *   h_i = SHA-256(Go-JSON(PrePrepareMsg i))                     -> out_digests; sig bit i
+ *   q_i = digest(embedded RequestMsg i) (Hash("null") if nil)   -> out_req_digests
+ *   msg bit i = verifyMsg(view_ids[i], sequence_ids[i], digest_i) with the state's
+ *               ReqMsg = the embedded request: view == state_view_ids[state_idx[i]]
+ *               && (last == -1 || last < sequence_ids[i]) && digest_i == hex(q_i)
+ *                                                               -> out_msg_bitmap
+ * (state_idx out of range -> 0). */
+int pbftv_flush_preprepares(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                            const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                            const uint8_t* has_request, const int64_t* req_timestamps, const uint8_t* req_client_ids,
+                            const uint64_t* req_client_id_off, const uint32_t* req_client_id_len,
+                            const uint8_t* req_operations, const uint64_t* req_operation_off,
+                            const uint32_t* req_operation_len, const int64_t* req_sequence_ids, const uint8_t* sig_rs,
+                            const uint32_t* key_idx, uint32_t n_states, const int64_t* state_view_ids,
+                            const int64_t* state_last_seqs, const uint32_t* state_idx, uint8_t* out_digests,
+                            uint8_t* out_req_digests, uint8_t* out_sig_bitmap, uint8_t* out_msg_bitmap);
 
 /* State.verifyMsg (pbft_impl.go:176-202) over n votes against one state:
  * bit i = view_ids[i] == state_view_id

@@ -89,13 +89,48 @@ def vote(view_id: int, sequence_id: int, digest: bytes, node_id: bytes, msg_type
             b',"nodeID":' + string(node_id) + b',"msgType":' + _int(msg_type) + b"}")
 
 
+def _bytes_field(b: bytes | None) -> bytes:
+    """encodeByteSlice (go1.19): base64.StdEncoding in quotes; a nil slice is null."""
+    import base64
+    return b"null" if b is None else b'"' + base64.b64encode(b) + b'"'
+
+
+def _with_signature(body: bytes, signature: bytes | None) -> bytes:
+    """A struct's encoding with the build-added last field Signature []byte `json:"signature"`."""
+    return body[:-1] + b',"signature":' + _bytes_field(signature) + b"}"
+
+
 def vote_signed(view_id: int, sequence_id: int, digest: bytes, node_id: bytes, msg_type: int,
                 signature: bytes | None) -> bytes:
     """Signed VoteMsg wire JSON (build-added field after the embedded MsgType):
     Go encodes a []byte as a base64.StdEncoding string and a nil slice as null."""
-    import base64
-    sig = b"null" if signature is None else b'"' + base64.b64encode(signature) + b'"'
-    return vote(view_id, sequence_id, digest, node_id, msg_type)[:-1] + b',"signature":' + sig + b"}"
+    return _with_signature(vote(view_id, sequence_id, digest, node_id, msg_type), signature)
+
+
+def request_signed(timestamp: int, client_id: bytes, operation: bytes, sequence_id: int,
+                   signature: bytes | None) -> bytes:
+    """Signed RequestMsg wire JSON."""
+    return _with_signature(request(timestamp, client_id, operation, sequence_id), signature)
+
+
+def reply_signed(view_id: int, timestamp: int, client_id: bytes, node_id: bytes, result: bytes,
+                 signature: bytes | None) -> bytes:
+    """Signed ReplyMsg wire JSON."""
+    return _with_signature(reply(view_id, timestamp, client_id, node_id, result), signature)
+
+
+def preprepare_signed(view_id: int, sequence_id: int, digest: bytes, req, req_signature: bytes | None,
+                      signature: bytes | None) -> bytes:
+    """Signed PrePrepareMsg wire JSON: the embedded request is the client's
+    signed RequestMsg (null if nil); the primary's signature is over preprepare() (unsigned)."""
+    body = request_signed(*req, req_signature) if req is not None else b"null"
+    return _with_signature(b'{"viewID":' + _int(view_id) + b',"sequenceID":' + _int(sequence_id) + b',"digest":' +
+                           string(digest) + b',"requestMsg":' + body + b"}", signature)
+
+
+def request_or_null(req) -> bytes:
+    """digest(*RequestMsg) preimage: json.Marshal of a nil pointer is null (pbft_impl.go:190)."""
+    return request(*req) if req is not None else b"null"
 
 
 def reply(view_id: int, timestamp: int, client_id: bytes, node_id: bytes, result: bytes) -> bytes:

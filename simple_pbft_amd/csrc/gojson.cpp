@@ -62,5 +62,24 @@ void append_preprepare(std::vector<uint8_t>& o, int64_t view, int64_t seq, const
   preprepare(k, view, seq, dg, dgn, has_req, rts, rcid, rcidn, rop, ropn, rseq);
 }
 
+void append_request_signed(std::vector<uint8_t>& o, int64_t ts, const uint8_t* cid, uint64_t cidn, const uint8_t* op,
+                           uint64_t opn, int64_t seq, const SigField& sig) {
+  VecSink k{o};
+  request_signed(k, ts, cid, cidn, op, opn, seq, sig);
+}
+
+void append_reply_signed(std::vector<uint8_t>& o, int64_t view, int64_t ts, const uint8_t* cid, uint64_t cidn,
+                         const uint8_t* nid, uint64_t nidn, const uint8_t* res, uint64_t resn, const SigField& sig) {
+  VecSink k{o};
+  reply_signed(k, view, ts, cid, cidn, nid, nidn, res, resn, sig);
+}
+
+void append_preprepare_signed(std::vector<uint8_t>& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t dgn,
+                              bool has_req, int64_t rts, const uint8_t* rcid, uint64_t rcidn, const uint8_t* rop,
+                              uint64_t ropn, int64_t rseq, const SigField& req_sig, const SigField& sig) {
+  VecSink k{o};
+  preprepare_signed(k, view, seq, dg, dgn, has_req, rts, rcid, rcidn, rop, ropn, rseq, req_sig, sig);
+}
+
 }  // namespace gojson
 }  // namespace pbftv

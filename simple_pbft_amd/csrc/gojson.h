@@ -9,6 +9,8 @@
 #include <cstdint>
 #include <vector>
 
+#include "gojson_enc.h"
+
 namespace pbftv {
 namespace gojson {
 
@@ -34,6 +36,19 @@ void append_preprepare(std::vector<uint8_t>& out, int64_t view_id, int64_t seque
                        uint64_t digest_len, bool has_request, int64_t req_timestamp, const uint8_t* req_client_id,
                        uint64_t req_client_id_len, const uint8_t* req_operation, uint64_t req_operation_len,
                        int64_t req_sequence_id);
+
+// signed wire encodings of the other three messages (gojson_enc.h)
+void append_request_signed(std::vector<uint8_t>& out, int64_t timestamp, const uint8_t* client_id,
+                           uint64_t client_id_len, const uint8_t* operation, uint64_t operation_len,
+                           int64_t sequence_id, const SigField& sig);
+void append_reply_signed(std::vector<uint8_t>& out, int64_t view_id, int64_t timestamp, const uint8_t* client_id,
+                         uint64_t client_id_len, const uint8_t* node_id, uint64_t node_id_len, const uint8_t* result,
+                         uint64_t result_len, const SigField& sig);
+void append_preprepare_signed(std::vector<uint8_t>& out, int64_t view_id, int64_t sequence_id, const uint8_t* digest,
+                              uint64_t digest_len, bool has_request, int64_t req_timestamp,
+                              const uint8_t* req_client_id, uint64_t req_client_id_len, const uint8_t* req_operation,
+                              uint64_t req_operation_len, int64_t req_sequence_id, const SigField& req_sig,
+                              const SigField& sig);
 
 }  // namespace gojson
 }  // namespace pbftv

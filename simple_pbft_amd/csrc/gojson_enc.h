@@ -178,9 +178,24 @@ PBFTV_GJ void put_bytes(S& o, const uint8_t* b, uint64_t n, bool is_nil) {
   o.put('"');
 }
 
-// Signed VoteMsg on the wire (build-added): the fields of
-// pbft_msg_types.go:25-31 followed by  Signature []byte `json:"signature"`.
-// The signing preimage is vote() above (the struct without the signature).
+// Signed messages on the wire (build-added): each struct of
+// pbft_msg_types.go:3-31 followed by  Signature []byte `json:"signature"`.  The
+// signing preimage of every message is its unsigned encoding (vote(),
+// request(), reply(), preprepare() here), i.e. the wire form up to the
+// signature field.
+struct SigField {
+  const uint8_t* p;
+  uint64_t n;
+  bool nil;
+};
+
+template <class S>
+PBFTV_GJ void put_sig_field(S& o, const SigField& s) {
+  lit(o, ",\"signature\":");
+  put_bytes(o, s.p, s.n, s.nil);
+  o.put('}');
+}
+
 template <class S>
 PBFTV_GJ void vote_signed(S& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t dgn, const uint8_t* nid,
                           uint64_t nidn, int64_t mt, const uint8_t* sig, uint64_t sign, bool sig_nil) {
@@ -194,9 +209,7 @@ PBFTV_GJ void vote_signed(S& o, int64_t view, int64_t seq, const uint8_t* dg, ui
   put_string(o, nid, nidn);
   lit(o, ",\"msgType\":");
   put_int(o, mt);
-  lit(o, ",\"signature\":");
-  put_bytes(o, sig, sign, sig_nil);
-  o.put('}');
+  put_sig_field(o, SigField{sig, sign, sig_nil});
 }
 
 // ReplyMsg (pbft_msg_types.go:10-16)
@@ -235,6 +248,69 @@ PBFTV_GJ void preprepare(S& o, int64_t view, int64_t seq, const uint8_t* dg, uin
 }
 PBFTV_GJ uint64_t preprepare_bound(uint64_t dgn, uint64_t rcidn, uint64_t ropn) {
   return 92 + 6 * dgn + request_bound(rcidn, ropn);
+}
+
+// digest(*RequestMsg) preimage for a possibly nil request: json.Marshal of a
+// nil pointer is "null" (pbft_impl.go:190 hashes state.MsgLogs.ReqMsg, which a
+// pre-prepare with requestMsg null leaves nil)
+template <class S>
+PBFTV_GJ void request_or_null(S& o, bool has, int64_t ts, const uint8_t* cid, uint64_t cidn, const uint8_t* op,
+                              uint64_t opn, int64_t seq) {
+  if (has) request(o, ts, cid, cidn, op, opn, seq);
+  else lit(o, "null");
+}
+
+// signed RequestMsg: the client's signature over request() as the client sent
+// it (sequenceID as given; the reference's clients leave it 0,
+// pbft_msg_types.go:7 and StartConsensus pbft_impl.go:67 assigns it later)
+template <class S>
+PBFTV_GJ void request_signed(S& o, int64_t ts, const uint8_t* cid, uint64_t cidn, const uint8_t* op, uint64_t opn,
+                             int64_t seq, const SigField& sig) {
+  lit(o, "{\"timestamp\":");
+  put_int(o, ts);
+  lit(o, ",\"clientID\":");
+  put_string(o, cid, cidn);
+  lit(o, ",\"operation\":");
+  put_string(o, op, opn);
+  lit(o, ",\"sequenceID\":");
+  put_int(o, seq);
+  put_sig_field(o, sig);
+}
+
+// signed ReplyMsg (the replying node's signature over reply())
+template <class S>
+PBFTV_GJ void reply_signed(S& o, int64_t view, int64_t ts, const uint8_t* cid, uint64_t cidn, const uint8_t* nid,
+                           uint64_t nidn, const uint8_t* res, uint64_t resn, const SigField& sig) {
+  lit(o, "{\"viewID\":");
+  put_int(o, view);
+  lit(o, ",\"timestamp\":");
+  put_int(o, ts);
+  lit(o, ",\"clientID\":");
+  put_string(o, cid, cidn);
+  lit(o, ",\"nodeID\":");
+  put_string(o, nid, nidn);
+  lit(o, ",\"result\":");
+  put_string(o, res, resn);
+  put_sig_field(o, sig);
+}
+
+// signed PrePrepareMsg: the primary's signature over preprepare() (the
+// embedded request unsigned: the digest field already commits to it); on the
+// wire the embedded request carries the client's signature (request_signed)
+template <class S>
+PBFTV_GJ void preprepare_signed(S& o, int64_t view, int64_t seq, const uint8_t* dg, uint64_t dgn, bool has_req,
+                                int64_t rts, const uint8_t* rcid, uint64_t rcidn, const uint8_t* rop, uint64_t ropn,
+                                int64_t rseq, const SigField& req_sig, const SigField& sig) {
+  lit(o, "{\"viewID\":");
+  put_int(o, view);
+  lit(o, ",\"sequenceID\":");
+  put_int(o, seq);
+  lit(o, ",\"digest\":");
+  put_string(o, dg, dgn);
+  lit(o, ",\"requestMsg\":");
+  if (has_req) request_signed(o, rts, rcid, rcidn, rop, ropn, rseq, req_sig);
+  else lit(o, "null");
+  put_sig_field(o, sig);
 }
 
 }  // namespace gojson

@@ -107,6 +107,46 @@ __global__ void __launch_bounds__(256) k_gojson_preprepare(PrePrepareCols c, uin
   out_len[i] = o.n;
 }
 
+// Pre-prepare flush: message i's preimage at slot[i] (signed by the primary)
+// and its embedded request's digest preimage at slot[n + i] ("null" for a nil
+// request, pbft_impl.go:93,190).
+__global__ void __launch_bounds__(256) k_gojson_preprepare_pair(PrePrepareCols c, uint64_t n,
+                                                                const uint64_t* __restrict__ slot,
+                                                                uint8_t* __restrict__ out,
+                                                                uint32_t* __restrict__ out_len) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool has = c.has_req[i] != 0;
+  const int64_t rts = has ? c.req.ts[i] : 0, rseq = has ? c.req.seq[i] : 0;
+  const uint32_t rcn = has ? c.req.cid.len[i] : 0, ron = has ? c.req.op.len[i] : 0;
+  DevSink o{out + slot[i], 0};
+  gojson::preprepare(o, c.view[i], c.seq[i], str(c.digest, i), c.digest.len[i], has, rts, str(c.req.cid, i), rcn,
+                     str(c.req.op, i), ron, rseq);
+  out_len[i] = o.n;
+  DevSink q{out + slot[n + i], 0};
+  gojson::request_or_null(q, has, rts, str(c.req.cid, i), rcn, str(c.req.op, i), ron, rseq);
+  out_len[n + i] = q.n;
+}
+
+// State.verifyMsg of pre-prepare i (PrePrepare, pbft_impl.go:91-97): the
+// replica's state takes the embedded request as its ReqMsg, so the digest
+// field is compared with the digest of that request (req_digests, 32 B each).
+__global__ void __launch_bounds__(256) k_preprepare_verify(const int64_t* __restrict__ view,
+                                                           const int64_t* __restrict__ seq, StrCol digest,
+                                                           const uint8_t* __restrict__ req_digests, StateCols s,
+                                                           uint64_t n, uint8_t* __restrict__ msg_ok) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t st = s.idx[i];
+  bool ok = st < s.n;
+  if (ok) {
+    const int64_t last = s.last_seq[st];
+    ok = view[i] == s.view[st] && (last == -1 || last < seq[i]) &&
+         hex_equals(str(digest, i), digest.len[i], req_digests + 32 * i);
+  }
+  msg_ok[i] = ok ? 1 : 0;
+}
+
 static inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 hipError_t launch_gojson_request(const RequestCols& c, uint64_t n, const uint64_t* slot, uint8_t* out,
@@ -134,6 +174,22 @@ hipError_t launch_gojson_preprepare(const PrePrepareCols& c, uint64_t n, const u
                                     uint32_t* out_len, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_gojson_preprepare, grid_for(n), dim3(256), 0, st, c, n, slot, out, out_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_gojson_preprepare_pair(const PrePrepareCols& c, uint64_t n, const uint64_t* slot, uint8_t* out,
+                                         uint32_t* out_len, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gojson_preprepare_pair, grid_for(n), dim3(256), 0, st, c, n, slot, out, out_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_preprepare_verify(const int64_t* view, const int64_t* seq, const StrCol& digest,
+                                   const uint8_t* req_digests, const StateCols& s, uint64_t n, uint8_t* msg_ok,
+                                   hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_preprepare_verify, grid_for(n), dim3(256), 0, st, view, seq, digest, req_digests, s, n,
+                     msg_ok);
   return hipGetLastError();
 }
 

@@ -151,5 +151,14 @@ hipError_t launch_gojson_reply(const ReplyCols& c, uint64_t n, const uint64_t* s
                                hipStream_t st);
 hipError_t launch_gojson_preprepare(const PrePrepareCols& c, uint64_t n, const uint64_t* slot, uint8_t* out,
                                     uint32_t* out_len, hipStream_t st);
+// pre-prepare flush: preimage i at slot[i], its embedded request's ("null" if
+// nil) at slot[n + i]; lengths likewise (out_len has 2n entries)
+hipError_t launch_gojson_preprepare_pair(const PrePrepareCols& c, uint64_t n, const uint64_t* slot, uint8_t* out,
+                                         uint32_t* out_len, hipStream_t st);
+// verifyMsg of pre-prepares against their states, the digest field compared
+// with the digest of the message's own request (req_digests, 32 B per message)
+hipError_t launch_preprepare_verify(const int64_t* view, const int64_t* seq, const StrCol& digest,
+                                   const uint8_t* req_digests, const StateCols& s, uint64_t n, uint8_t* msg_ok,
+                                   hipStream_t st);
 
 }  // namespace pbftv

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <initializer_list>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -446,13 +447,64 @@ int encode_and_hash(Device& d, uint64_t m, const uint64_t* slot_dev, uint64_t pr
   return PBFTV_OK;
 }
 
-// digests of shard [lo, hi) back to the caller
-int digests_out(Device& d, uint64_t lo, uint64_t m, uint8_t* out) {
-  HIP_TRY(d.mout.ensure(m * 32 + 32));
-  HIP_TRY(hipMemcpyAsync(d.mout.p, d.digests.p, m * 32, hipMemcpyDeviceToHost, d.stream));
+// Results of one flush shard [lo, lo + m), copied back in ONE device -> host
+// round trip through pinned staging: 32-B digests, a device bitmap (tail bits
+// past the shard masked), or one flag byte per item packed into bits.
+enum OutKind { kDigests, kBitmap, kByteFlags };
+struct OutSeg {
+  OutKind kind;
+  const void* dev;
+  uint8_t* host;  // the caller's whole-batch buffer (null: not requested)
+};
+
+int results_out(Device& d, uint64_t lo, uint64_t m, std::initializer_list<OutSeg> segs) {
+  const uint64_t nb = (m + 7) / 8;
+  auto bytes = [&](OutKind k) -> uint64_t { return k == kDigests ? 32 * m : (k == kBitmap ? nb : m); };
+  size_t total = 0;
+  for (const auto& g : segs)
+    if (g.host) total += (bytes(g.kind) + 15) & ~(uint64_t)15;
+  if (total == 0) return PBFTV_OK;
+  HIP_TRY(d.mout.ensure(total + 16));
+  uint8_t* h = d.mout.as<uint8_t>();
+  size_t off = 0;
+  for (const auto& g : segs) {
+    if (!g.host) continue;
+    HIP_TRY(hipMemcpyAsync(h + off, g.dev, bytes(g.kind), hipMemcpyDeviceToHost, d.stream));
+    off += (bytes(g.kind) + 15) & ~(uint64_t)15;
+  }
   HIP_TRY(hipStreamSynchronize(d.stream));
-  std::memcpy(out + 32 * lo, d.mout.p, m * 32);
+  off = 0;
+  for (const auto& g : segs) {
+    if (!g.host) continue;
+    const uint8_t* src = h + off;
+    if (g.kind == kDigests) {
+      std::memcpy(g.host + 32 * lo, src, 32 * m);
+    } else if (g.kind == kBitmap) {
+      std::memcpy(g.host + lo / 8, src, nb);
+      if (m % 8) g.host[lo / 8 + nb - 1] &= (uint8_t)((1u << (m % 8)) - 1u);
+    } else {
+      uint8_t* bm = g.host + lo / 8;
+      std::memset(bm, 0, nb);
+      for (uint64_t i = 0; i < m; ++i) bm[i >> 3] |= (uint8_t)((src[i] & 1u) << (i & 7));
+    }
+    off += (bytes(g.kind) + 15) & ~(uint64_t)15;
+  }
   return PBFTV_OK;
+}
+
+// the same slot layout twice: a second preimage set right after the first
+std::vector<uint64_t> twice(std::vector<uint64_t> s, uint64_t* total) {
+  const size_t m = s.size();
+  s.resize(2 * m);
+  for (size_t i = 0; i < m; ++i) s[m + i] = s[i] + *total;
+  *total *= 2;
+  return s;
+}
+
+bool keys_ready(pbftv_ctx* ctx) {
+  for (auto& dp : ctx->devs)
+    if (!dp->have_keys) return false;
+  return true;
 }
 
 }  // namespace
@@ -1121,56 +1173,96 @@ int pbftv_hash_hex(pbftv_ctx* ctx, const uint8_t* content, uint64_t len, char ou
   return PBFTV_OK;
 }
 
-// ---- digests of message batches: Go-JSON built on the device, then SHA-256 ----
-int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
-                               const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
-                               const uint64_t* operation_off, const uint32_t* operation_len,
-                               const int64_t* sequence_ids, uint8_t* out_digests) {
+// ---- message batches: Go-JSON built on the device, SHA-256, signatures ----
+// Every entry point below is one device round trip per shard: the columns go
+// up in one H2D copy (Packer), the encoder kernel writes the Go-JSON preimages,
+// k_sha256 hashes them, the signature stage runs on the digests in HBM, and
+// the results come back in one D2H copy.  The digest_*_batch functions are the
+// flushes with no signatures.
+int pbftv_flush_requests(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
+                         const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
+                         const uint64_t* operation_off, const uint32_t* operation_len, const int64_t* sequence_ids,
+                         const uint8_t* sig_rs, const uint32_t* key_idx, const int64_t* assigned_seqs,
+                         uint8_t* out_digests, uint8_t* out_sig_bitmap, uint8_t* out_consensus_digests) {
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
-  if (n && (!timestamps || !client_id_off || !client_id_len || !operation_off || !operation_len || !sequence_ids ||
-            !out_digests))
+  if (n && (!timestamps || !client_id_off || !client_id_len || !operation_off || !operation_len || !sequence_ids))
     return fail(PBFTV_EINVAL, "null buffer");
+  const bool sig = out_sig_bitmap != nullptr, two = out_consensus_digests != nullptr;
+  if (n && sig && (!sig_rs || !key_idx)) return fail(PBFTV_EINVAL, "signatures requested without sig_rs/key_idx");
+  if (n && two && !assigned_seqs) return fail(PBFTV_EINVAL, "consensus digests requested without assigned_seqs");
+  if (sig && !keys_ready(ctx)) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
     const uint64_t m = s.hi - s.lo;
     Packer p;
     uint64_t pre = 0;
-    const size_t o_slot = p.add_owned(slots(s.lo, s.hi, [&](uint64_t i) {
+    auto sl = slots(s.lo, s.hi, [&](uint64_t i) {
       return pbftv::gojson::request_bound(client_id_len[i], operation_len[i]);
-    }, &pre));
+    }, &pre);
+    const size_t o_slot = p.add_owned(two ? twice(std::move(sl), &pre) : std::move(sl));
     const size_t o_ts = p.add(timestamps + s.lo, 8 * m), o_seq = p.add(sequence_ids + s.lo, 8 * m);
+    const size_t o_aseq = two ? p.add(assigned_seqs + s.lo, 8 * m) : 0;
     const auto cid = p.add_str(client_ids, client_id_off, client_id_len, s.lo, s.hi);
     const auto op = p.add_str(operations, operation_off, operation_len, s.lo, s.hi);
+    const size_t o_sig = sig ? p.add(sig_rs + 64 * s.lo, 64 * m) : 0, o_key = sig ? p.add(key_idx + s.lo, 4 * m) : 0;
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
     int rc = upload(d, p);
     if (rc != PBFTV_OK) return rc;
     const pbftv::RequestCols c{at<int64_t>(d, o_ts), str_col(d, cid), str_col(d, op), at<int64_t>(d, o_seq)};
     const uint64_t* slot = at<uint64_t>(d, o_slot);
-    rc = encode_and_hash(d, m, slot, pre, [&] {
-      return pbftv::launch_gojson_request(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), d.stream);
+    rc = encode_and_hash(d, two ? 2 * m : m, slot, pre, [&] {
+      hipError_t e = pbftv::launch_gojson_request(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), d.stream);
+      if (e != hipSuccess || !two) return e;
+      pbftv::RequestCols c2 = c;  // StartConsensus digest: SequenceID assigned (pbft_impl.go:67-73)
+      c2.seq = at<int64_t>(d, o_aseq);
+      return pbftv::launch_gojson_request(c2, m, slot + m, d.data.as<uint8_t>(), d.lengths.as<uint32_t>() + m,
+                                          d.stream);
     });
-    return rc != PBFTV_OK ? rc : digests_out(d, s.lo, m, out_digests);
+    if (rc != PBFTV_OK) return rc;
+    if (sig) {
+      HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
+      rc = verify_on_device(d, d.digests.as<uint8_t>(), at<uint8_t>(d, o_sig), at<uint32_t>(d, o_key), m,
+                            d.bitmap.as<uint8_t>(), d.stream);
+      if (rc != PBFTV_OK) return rc;
+    }
+    return results_out(d, s.lo, m, {{kDigests, d.digests.p, out_digests},
+                                    {kDigests, d.digests.as<uint8_t>() + 32 * m, out_consensus_digests},
+                                    {kBitmap, d.bitmap.p, sig ? out_sig_bitmap : nullptr}});
   });
+}
+
+int pbftv_digest_request_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* timestamps, const uint8_t* client_ids,
+                               const uint64_t* client_id_off, const uint32_t* client_id_len, const uint8_t* operations,
+                               const uint64_t* operation_off, const uint32_t* operation_len,
+                               const int64_t* sequence_ids, uint8_t* out_digests) {
+  if (n && !out_digests) return fail(PBFTV_EINVAL, "null buffer");
+  return pbftv_flush_requests(ctx, n, timestamps, client_ids, client_id_off, client_id_len, operations, operation_off,
+                              operation_len, sequence_ids, nullptr, nullptr, nullptr, out_digests, nullptr, nullptr);
 }
 
 int pbftv_digest_vote_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
                             const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
                             const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
                             const int64_t* msg_types, uint8_t* out_digests) {
+  if (n && !out_digests) return fail(PBFTV_EINVAL, "null buffer");
   return pbftv_flush_votes(ctx, n, view_ids, sequence_ids, digests, digest_off, digest_len, node_ids, node_id_off,
                            node_id_len, msg_types, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
                            out_digests, nullptr, nullptr);
 }
 
-int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* timestamps,
-                             const uint8_t* client_ids, const uint64_t* client_id_off, const uint32_t* client_id_len,
-                             const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
-                             const uint8_t* results, const uint64_t* result_off, const uint32_t* result_len,
-                             uint8_t* out_digests) {
+int pbftv_flush_replies(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* timestamps,
+                        const uint8_t* client_ids, const uint64_t* client_id_off, const uint32_t* client_id_len,
+                        const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                        const uint8_t* results, const uint64_t* result_off, const uint32_t* result_len,
+                        const uint8_t* sig_rs, const uint32_t* key_idx, uint8_t* out_digests,
+                        uint8_t* out_sig_bitmap) {
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
   if (n && (!view_ids || !timestamps || !client_id_off || !client_id_len || !node_id_off || !node_id_len ||
-            !result_off || !result_len || !out_digests))
+            !result_off || !result_len))
     return fail(PBFTV_EINVAL, "null buffer");
+  const bool sig = out_sig_bitmap != nullptr;
+  if (n && sig && (!sig_rs || !key_idx)) return fail(PBFTV_EINVAL, "signatures requested without sig_rs/key_idx");
+  if (sig && !keys_ready(ctx)) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
     const uint64_t m = s.hi - s.lo;
     Packer p;
@@ -1182,6 +1274,7 @@ int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids
     const auto cid = p.add_str(client_ids, client_id_off, client_id_len, s.lo, s.hi);
     const auto nid = p.add_str(node_ids, node_id_off, node_id_len, s.lo, s.hi);
     const auto res = p.add_str(results, result_off, result_len, s.lo, s.hi);
+    const size_t o_sig = sig ? p.add(sig_rs + 64 * s.lo, 64 * m) : 0, o_key = sig ? p.add(key_idx + s.lo, 4 * m) : 0;
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
     int rc = upload(d, p);
@@ -1192,7 +1285,115 @@ int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids
     rc = encode_and_hash(d, m, slot, pre, [&] {
       return pbftv::launch_gojson_reply(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), d.stream);
     });
-    return rc != PBFTV_OK ? rc : digests_out(d, s.lo, m, out_digests);
+    if (rc != PBFTV_OK) return rc;
+    if (sig) {
+      HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
+      rc = verify_on_device(d, d.digests.as<uint8_t>(), at<uint8_t>(d, o_sig), at<uint32_t>(d, o_key), m,
+                            d.bitmap.as<uint8_t>(), d.stream);
+      if (rc != PBFTV_OK) return rc;
+    }
+    return results_out(d, s.lo, m, {{kDigests, d.digests.p, out_digests},
+                                    {kBitmap, d.bitmap.p, sig ? out_sig_bitmap : nullptr}});
+  });
+}
+
+int pbftv_digest_reply_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* timestamps,
+                             const uint8_t* client_ids, const uint64_t* client_id_off, const uint32_t* client_id_len,
+                             const uint8_t* node_ids, const uint64_t* node_id_off, const uint32_t* node_id_len,
+                             const uint8_t* results, const uint64_t* result_off, const uint32_t* result_len,
+                             uint8_t* out_digests) {
+  if (n && !out_digests) return fail(PBFTV_EINVAL, "null buffer");
+  return pbftv_flush_replies(ctx, n, view_ids, timestamps, client_ids, client_id_off, client_id_len, node_ids,
+                             node_id_off, node_id_len, results, result_off, result_len, nullptr, nullptr, out_digests,
+                             nullptr);
+}
+
+int pbftv_flush_preprepares(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const int64_t* sequence_ids,
+                            const uint8_t* digests, const uint64_t* digest_off, const uint32_t* digest_len,
+                            const uint8_t* has_request, const int64_t* req_timestamps, const uint8_t* req_client_ids,
+                            const uint64_t* req_client_id_off, const uint32_t* req_client_id_len,
+                            const uint8_t* req_operations, const uint64_t* req_operation_off,
+                            const uint32_t* req_operation_len, const int64_t* req_sequence_ids, const uint8_t* sig_rs,
+                            const uint32_t* key_idx, uint32_t n_states, const int64_t* state_view_ids,
+                            const int64_t* state_last_seqs, const uint32_t* state_idx, uint8_t* out_digests,
+                            uint8_t* out_req_digests, uint8_t* out_sig_bitmap, uint8_t* out_msg_bitmap) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  if (n && (!view_ids || !sequence_ids || !digest_off || !digest_len || !has_request || !req_timestamps ||
+            !req_client_id_off || !req_client_id_len || !req_operation_off || !req_operation_len ||
+            !req_sequence_ids))
+    return fail(PBFTV_EINVAL, "null buffer");
+  const bool sig = out_sig_bitmap != nullptr, msg = out_msg_bitmap != nullptr;
+  if (n && sig && (!sig_rs || !key_idx)) return fail(PBFTV_EINVAL, "signatures requested without sig_rs/key_idx");
+  if (n && msg && (!state_idx || (n_states && (!state_view_ids || !state_last_seqs))))
+    return fail(PBFTV_EINVAL, "verifyMsg requested without states");
+  if (sig && !keys_ready(ctx)) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  // the embedded requests' digests are needed for verifyMsg or when asked for
+  const bool pair = msg || out_req_digests != nullptr;
+  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
+    const uint64_t m = s.hi - s.lo;
+    Packer p;
+    uint64_t pre = 0;
+    auto rb = [&](uint64_t i) {
+      return has_request[i] ? pbftv::gojson::request_bound(req_client_id_len[i], req_operation_len[i]) : 4;
+    };
+    auto sl = slots(s.lo, s.hi, [&](uint64_t i) {
+      return pbftv::gojson::preprepare_bound(digest_len[i], has_request[i] ? req_client_id_len[i] : 0,
+                                             has_request[i] ? req_operation_len[i] : 0);
+    }, &pre);
+    if (pair) {  // request preimages in slots [m, 2m)
+      uint64_t pre2 = 0;
+      auto s2 = slots(s.lo, s.hi, rb, &pre2);
+      sl.resize(2 * m);
+      for (uint64_t i = 0; i < m; ++i) sl[m + i] = pre + s2[i];
+      pre += pre2;
+    }
+    const size_t o_slot = p.add_owned(std::move(sl));
+    const size_t o_view = p.add(view_ids + s.lo, 8 * m), o_seq = p.add(sequence_ids + s.lo, 8 * m);
+    const size_t o_has = p.add(has_request + s.lo, m);
+    const size_t o_rts = p.add(req_timestamps + s.lo, 8 * m), o_rseq = p.add(req_sequence_ids + s.lo, 8 * m);
+    const auto dg = p.add_str(digests, digest_off, digest_len, s.lo, s.hi);
+    const auto cid = p.add_str(req_client_ids, req_client_id_off, req_client_id_len, s.lo, s.hi);
+    const auto op = p.add_str(req_operations, req_operation_off, req_operation_len, s.lo, s.hi);
+    const size_t o_sig = sig ? p.add(sig_rs + 64 * s.lo, 64 * m) : 0, o_key = sig ? p.add(key_idx + s.lo, 4 * m) : 0;
+    size_t o_sv = 0, o_sl = 0, o_si = 0;
+    if (msg) {
+      o_sv = p.add(state_view_ids, 8ull * n_states);
+      o_sl = p.add(state_last_seqs, 8ull * n_states);
+      o_si = p.add(state_idx + s.lo, 4 * m);
+    }
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    int rc = upload(d, p);
+    if (rc != PBFTV_OK) return rc;
+    const pbftv::PrePrepareCols c{
+        at<int64_t>(d, o_view), at<int64_t>(d, o_seq), str_col(d, dg), at<uint8_t>(d, o_has),
+        {at<int64_t>(d, o_rts), str_col(d, cid), str_col(d, op), at<int64_t>(d, o_rseq)}};
+    const uint64_t* slot = at<uint64_t>(d, o_slot);
+    rc = encode_and_hash(d, pair ? 2 * m : m, slot, pre, [&] {
+      return pair ? pbftv::launch_gojson_preprepare_pair(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(),
+                                                         d.stream)
+                  : pbftv::launch_gojson_preprepare(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(),
+                                                    d.stream);
+    });
+    if (rc != PBFTV_OK) return rc;
+    if (sig) {
+      HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
+      rc = verify_on_device(d, d.digests.as<uint8_t>(), at<uint8_t>(d, o_sig), at<uint32_t>(d, o_key), m,
+                            d.bitmap.as<uint8_t>(), d.stream);
+      if (rc != PBFTV_OK) return rc;
+    }
+    uint8_t* msgok = nullptr;
+    if (msg) {
+      HIP_TRY(d.msgok.ensure(m + 8));
+      msgok = d.msgok.as<uint8_t>();
+      const pbftv::StateCols sc{at<int64_t>(d, o_sv), at<int64_t>(d, o_sl), nullptr, at<uint32_t>(d, o_si), n_states};
+      HIP_TRY(pbftv::launch_preprepare_verify(c.view, c.seq, c.digest, d.digests.as<uint8_t>() + 32 * m, sc, m, msgok,
+                                             d.stream));
+    }
+    return results_out(d, s.lo, m, {{kDigests, d.digests.p, out_digests},
+                                    {kDigests, d.digests.as<uint8_t>() + 32 * m, pair ? out_req_digests : nullptr},
+                                    {kBitmap, d.bitmap.p, sig ? out_sig_bitmap : nullptr},
+                                    {kByteFlags, msgok, out_msg_bitmap}});
   });
 }
 
@@ -1203,38 +1404,11 @@ int pbftv_digest_preprepare_batch(pbftv_ctx* ctx, uint64_t n, const int64_t* vie
                                   const uint32_t* req_client_id_len, const uint8_t* req_operations,
                                   const uint64_t* req_operation_off, const uint32_t* req_operation_len,
                                   const int64_t* req_sequence_ids, uint8_t* out_digests) {
-  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
-  if (n && (!view_ids || !sequence_ids || !digest_off || !digest_len || !has_request || !req_timestamps ||
-            !req_client_id_off || !req_client_id_len || !req_operation_off || !req_operation_len ||
-            !req_sequence_ids || !out_digests))
-    return fail(PBFTV_EINVAL, "null buffer");
-  return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
-    const uint64_t m = s.hi - s.lo;
-    Packer p;
-    uint64_t pre = 0;
-    const size_t o_slot = p.add_owned(slots(s.lo, s.hi, [&](uint64_t i) {
-      return pbftv::gojson::preprepare_bound(digest_len[i], has_request[i] ? req_client_id_len[i] : 0,
-                                             has_request[i] ? req_operation_len[i] : 0);
-    }, &pre));
-    const size_t o_view = p.add(view_ids + s.lo, 8 * m), o_seq = p.add(sequence_ids + s.lo, 8 * m);
-    const size_t o_has = p.add(has_request + s.lo, m);
-    const size_t o_rts = p.add(req_timestamps + s.lo, 8 * m), o_rseq = p.add(req_sequence_ids + s.lo, 8 * m);
-    const auto dg = p.add_str(digests, digest_off, digest_len, s.lo, s.hi);
-    const auto cid = p.add_str(req_client_ids, req_client_id_off, req_client_id_len, s.lo, s.hi);
-    const auto op = p.add_str(req_operations, req_operation_off, req_operation_len, s.lo, s.hi);
-    std::lock_guard<std::mutex> lk(d.mu);
-    HIP_TRY(hipSetDevice(d.id));
-    int rc = upload(d, p);
-    if (rc != PBFTV_OK) return rc;
-    const pbftv::PrePrepareCols c{
-        at<int64_t>(d, o_view), at<int64_t>(d, o_seq), str_col(d, dg), at<uint8_t>(d, o_has),
-        {at<int64_t>(d, o_rts), str_col(d, cid), str_col(d, op), at<int64_t>(d, o_rseq)}};
-    const uint64_t* slot = at<uint64_t>(d, o_slot);
-    rc = encode_and_hash(d, m, slot, pre, [&] {
-      return pbftv::launch_gojson_preprepare(c, m, slot, d.data.as<uint8_t>(), d.lengths.as<uint32_t>(), d.stream);
-    });
-    return rc != PBFTV_OK ? rc : digests_out(d, s.lo, m, out_digests);
-  });
+  if (n && !out_digests) return fail(PBFTV_EINVAL, "null buffer");
+  return pbftv_flush_preprepares(ctx, n, view_ids, sequence_ids, digests, digest_off, digest_len, has_request,
+                                 req_timestamps, req_client_ids, req_client_id_off, req_client_id_len, req_operations,
+                                 req_operation_off, req_operation_len, req_sequence_ids, nullptr, nullptr, 0, nullptr,
+                                 nullptr, nullptr, out_digests, nullptr, nullptr, nullptr);
 }
 
 // Pool flush of a vote snapshot: Go-JSON + SHA-256 + verifyMsg + ECDSA in one
@@ -1254,9 +1428,7 @@ int pbftv_flush_votes(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const
   if (n && sig && (!sig_rs || !key_idx)) return fail(PBFTV_EINVAL, "signatures requested without sig_rs/key_idx");
   if (n && msg && (!state_idx || (n_states && (!state_view_ids || !state_last_seqs || !state_req_digests))))
     return fail(PBFTV_EINVAL, "verifyMsg requested without states");
-  if (sig)
-    for (auto& dp : ctx->devs)
-      if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  if (sig && !keys_ready(ctx)) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
     const uint64_t m = s.hi - s.lo;
     Packer p;
@@ -1298,32 +1470,15 @@ int pbftv_flush_votes(pbftv_ctx* ctx, uint64_t n, const int64_t* view_ids, const
                                        d.stream);
     });
     if (rc != PBFTV_OK) return rc;
-    const uint64_t nb = (m + 7) / 8;
     if (sig) {
-      HIP_TRY(d.bitmap.ensure(nb + 8));
+      HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
       rc = verify_on_device(d, d.digests.as<uint8_t>(), at<uint8_t>(d, o_sig), at<uint32_t>(d, o_key), m,
                             d.bitmap.as<uint8_t>(), d.stream);
       if (rc != PBFTV_OK) return rc;
     }
-    // results: digests | signature bitmap | verifyMsg bytes
-    const size_t r_dg = 0, r_sig = out_digests ? 32 * m : 0, r_msg = r_sig + (sig ? nb : 0);
-    HIP_TRY(d.mout.ensure(r_msg + (msg ? m : 0) + 16));
-    uint8_t* h = d.mout.as<uint8_t>();
-    if (out_digests) HIP_TRY(hipMemcpyAsync(h + r_dg, d.digests.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
-    if (sig) HIP_TRY(hipMemcpyAsync(h + r_sig, d.bitmap.p, nb, hipMemcpyDeviceToHost, d.stream));
-    if (msg) HIP_TRY(hipMemcpyAsync(h + r_msg, msgok, m, hipMemcpyDeviceToHost, d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));
-    if (out_digests) std::memcpy(out_digests + 32 * s.lo, h + r_dg, 32 * m);
-    if (sig) {
-      std::memcpy(out_sig_bitmap + s.lo / 8, h + r_sig, nb);
-      if (m % 8) out_sig_bitmap[s.lo / 8 + nb - 1] &= (uint8_t)((1u << (m % 8)) - 1u);
-    }
-    if (msg) {
-      uint8_t* bm = out_msg_bitmap + s.lo / 8;
-      std::memset(bm, 0, nb);
-      for (uint64_t i = 0; i < m; ++i) bm[i >> 3] |= (uint8_t)((h[r_msg + i] & 1u) << (i & 7));
-    }
-    return PBFTV_OK;
+    return results_out(d, s.lo, m, {{kDigests, d.digests.p, out_digests},
+                                    {kBitmap, d.bitmap.p, sig ? out_sig_bitmap : nullptr},
+                                    {kByteFlags, msgok, out_msg_bitmap}});
   });
 }
 
@@ -1374,6 +1529,49 @@ uint64_t pbftv_gojson_vote_signed(int64_t view_id, int64_t sequence_id, const ch
   pbftv::gojson::append_vote_signed(b, view_id, sequence_id, reinterpret_cast<const uint8_t*>(digest), digest_len,
                                     reinterpret_cast<const uint8_t*>(node_id), node_id_len, msg_type, sig, sig_len,
                                     sig_nil != 0);
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
+static pbftv::gojson::SigField sig_field(const uint8_t* sig, uint64_t sig_len, int sig_nil) {
+  return {sig, sig_len, sig_nil != 0};
+}
+
+uint64_t pbftv_gojson_request_signed(int64_t timestamp, const char* client_id, uint64_t client_id_len,
+                                     const char* operation, uint64_t operation_len, int64_t sequence_id,
+                                     const uint8_t* sig, uint64_t sig_len, int sig_nil, uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_request_signed(b, timestamp, reinterpret_cast<const uint8_t*>(client_id), client_id_len,
+                                       reinterpret_cast<const uint8_t*>(operation), operation_len, sequence_id,
+                                       sig_field(sig, sig_len, sig_nil));
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
+uint64_t pbftv_gojson_reply_signed(int64_t view_id, int64_t timestamp, const char* client_id, uint64_t client_id_len,
+                                   const char* node_id, uint64_t node_id_len, const char* result, uint64_t result_len,
+                                   const uint8_t* sig, uint64_t sig_len, int sig_nil, uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_reply_signed(b, view_id, timestamp, reinterpret_cast<const uint8_t*>(client_id),
+                                     client_id_len, reinterpret_cast<const uint8_t*>(node_id), node_id_len,
+                                     reinterpret_cast<const uint8_t*>(result), result_len,
+                                     sig_field(sig, sig_len, sig_nil));
+  if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
+  return b.size();
+}
+
+uint64_t pbftv_gojson_preprepare_signed(int64_t view_id, int64_t sequence_id, const char* digest, uint64_t digest_len,
+                                        int has_request, int64_t req_timestamp, const char* req_client_id,
+                                        uint64_t req_client_id_len, const char* req_operation,
+                                        uint64_t req_operation_len, int64_t req_sequence_id, const uint8_t* req_sig,
+                                        uint64_t req_sig_len, int req_sig_nil, const uint8_t* sig, uint64_t sig_len,
+                                        int sig_nil, uint8_t* out, uint64_t cap) {
+  std::vector<uint8_t> b;
+  pbftv::gojson::append_preprepare_signed(
+      b, view_id, sequence_id, reinterpret_cast<const uint8_t*>(digest), digest_len, has_request != 0, req_timestamp,
+      reinterpret_cast<const uint8_t*>(req_client_id), req_client_id_len,
+      reinterpret_cast<const uint8_t*>(req_operation), req_operation_len, req_sequence_id,
+      sig_field(req_sig, req_sig_len, req_sig_nil), sig_field(sig, sig_len, sig_nil));
   if (out) std::memcpy(out, b.data(), std::min<uint64_t>(cap, b.size()));
   return b.size();
 }

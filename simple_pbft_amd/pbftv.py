@@ -87,6 +87,24 @@ def lib() -> ctypes.CDLL:
                                                        ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                                        ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
                                                        _vp, ctypes.c_uint64]),
+        "pbftv_gojson_request_signed": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64,
+                                                          ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int64,
+                                                          ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, _vp,
+                                                          ctypes.c_uint64]),
+        "pbftv_gojson_reply_signed": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p,
+                                                        ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                                                        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p,
+                                                        ctypes.c_uint64, ctypes.c_int, _vp, ctypes.c_uint64]),
+        "pbftv_gojson_preprepare_signed": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p,
+                                                             ctypes.c_uint64, ctypes.c_int, ctypes.c_int64,
+                                                             ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p,
+                                                             ctypes.c_uint64, ctypes.c_int64, ctypes.c_char_p,
+                                                             ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p,
+                                                             ctypes.c_uint64, ctypes.c_int, _vp, ctypes.c_uint64]),
+        "pbftv_flush_requests": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 14),
+        "pbftv_flush_replies": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 15),
+        "pbftv_flush_preprepares": (ctypes.c_int, [_vp, ctypes.c_uint64] + [_vp] * 16 + [ctypes.c_uint32] +
+                                    [_vp] * 7),
         "pbftv_ecdsa_der_to_rs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _vp]),
         "pbftv_ecdsa_der_to_rs_batch": (ctypes.c_int64, [_vp, _vp, _vp, ctypes.c_uint64, _vp]),
         "pbftv_gojson_reply": (ctypes.c_uint64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint64,
@@ -178,6 +196,44 @@ def gojson_vote_signed(view: int, seq: int, digest: bytes, node_id: bytes, msg_t
     buf = np.zeros(max(n, 1), np.uint8)
     L.pbftv_gojson_vote_signed(*args, buf.ctypes.data, n)
     return buf[:n].tobytes()
+
+
+def _sig_args(signature: bytes | None):
+    sig = signature if signature is not None else b""
+    return sig, len(sig), 1 if signature is None else 0
+
+
+def _encode(fn, *args) -> bytes:
+    n = fn(*args, None, 0)
+    buf = np.zeros(max(n, 1), np.uint8)
+    fn(*args, buf.ctypes.data, n)
+    return buf[:n].tobytes()
+
+
+def gojson_request_signed(ts: int, client_id: bytes, operation: bytes, seq: int, signature: bytes | None) -> bytes:
+    """Signed RequestMsg wire JSON: RequestMsg + "signature" (base64, None -> null)."""
+    return _encode(lib().pbftv_gojson_request_signed, ts, client_id, len(client_id), operation, len(operation), seq,
+                   *_sig_args(signature))
+
+
+def gojson_reply_signed(view: int, ts: int, client_id: bytes, node_id: bytes, result: bytes,
+                        signature: bytes | None) -> bytes:
+    """Signed ReplyMsg wire JSON."""
+    return _encode(lib().pbftv_gojson_reply_signed, view, ts, client_id, len(client_id), node_id, len(node_id),
+                   result, len(result), *_sig_args(signature))
+
+
+def gojson_preprepare_signed(view: int, seq: int, digest: bytes, req, req_signature: bytes | None,
+                             signature: bytes | None) -> bytes:
+    """Signed PrePrepareMsg wire JSON; req = (ts, clientID, op, seq) or None, the
+    embedded request carrying the client's signature req_signature."""
+    if req is None:
+        r = (0, 0, b"", 0, b"", 0, 0)
+    else:
+        ts, cid, op, rseq = req
+        r = (1, ts, cid, len(cid), op, len(op), rseq)
+    return _encode(lib().pbftv_gojson_preprepare_signed, view, seq, digest, len(digest), *r,
+                   *_sig_args(req_signature), *_sig_args(signature))
 
 
 def der_to_rs(der: bytes) -> bytes | None:
@@ -307,6 +363,53 @@ class VoteColumns:
         (db, do, dl), (nb, no, nl) = self.digest, self.node
         return [self.view.ctypes.data, self.seq.ctypes.data, db.ctypes.data, do.ctypes.data, dl.ctypes.data,
                 nb.ctypes.data, no.ctypes.data, nl.ctypes.data, self.type.ctypes.data]
+
+
+class PrePrepareColumns:
+    """PrePrepareMsgs (pbft_msg_types.go:18-23) column-wise: request None -> requestMsg null
+    (its request columns still hold a placeholder row)."""
+
+    def __init__(self, pps):
+        """pps: list of (viewID, sequenceID, digest bytes, request) with request None or
+        (timestamp, clientID bytes, operation bytes, sequenceID)."""
+        self.n = len(pps)
+        self.view = np.array([x[0] for x in pps], np.int64)
+        self.seq = np.array([x[1] for x in pps], np.int64)
+        self.has = np.array([x[3] is not None for x in pps], np.uint8)
+        reqs = [x[3] if x[3] is not None else (0, b"", b"", 0) for x in pps]
+        self.rts = np.array([r[0] for r in reqs], np.int64)
+        self.rseq = np.array([r[3] for r in reqs], np.int64)
+        self.digest = Verifier.pack([x[2] for x in pps])
+        self.cid = Verifier.pack([r[1] for r in reqs])
+        self.op = Verifier.pack([r[2] for r in reqs])
+
+    def args(self):
+        (db, do, dl), (cb, co, cl), (ob, oo, ol) = self.digest, self.cid, self.op
+        return [self.view.ctypes.data, self.seq.ctypes.data, db.ctypes.data, do.ctypes.data, dl.ctypes.data,
+                self.has.ctypes.data, self.rts.ctypes.data, cb.ctypes.data, co.ctypes.data, cl.ctypes.data,
+                ob.ctypes.data, oo.ctypes.data, ol.ctypes.data, self.rseq.ctypes.data]
+
+
+def _sig_inputs(n: int, sigs, key_idx, what: str):
+    if sigs is None:
+        return None, None, None
+    sigs = np.ascontiguousarray(sigs, np.uint8)
+    key_idx = np.ascontiguousarray(key_idx, np.uint32)
+    if sigs.shape != (n, 64) or key_idx.shape != (n,):
+        raise ValueError(f"{what}: sigs must be (n, 64) uint8 and key_idx (n,)")
+    return sigs, key_idx, np.zeros((n + 7) // 8 + 1, np.uint8)
+
+
+def _states(n: int, states, state_idx, what: str, with_digests: bool):
+    sv = np.ascontiguousarray(states[0], np.int64)
+    sl = np.ascontiguousarray(states[1], np.int64)
+    si = np.ascontiguousarray(state_idx, np.uint32)
+    k = len(sv)
+    sd = np.ascontiguousarray(states[2], np.uint8) if with_digests else None
+    if sl.shape != (k,) or si.shape != (n,) or (with_digests and sd.shape != (k, 32)):
+        raise ValueError(f"{what}: states must be (k,), (k,){', (k, 32)' if with_digests else ''} "
+                         "and state_idx (n,)")
+    return k, sv, sl, sd, si
 
 
 class DeviceBuffer:
@@ -549,6 +652,49 @@ class Verifier:
         _check(self._L.pbftv_flush_votes(self._h, n, *cols.args(), sp, kp, k, svp, slp, sdp, sip,
                                          _ptr(out_d), _ptr(sbm), _ptr(mbm)))
         return (out_d[:n] if digests else None, bitmap_to_bool(sbm, n) if sbm is not None else None,
+                bitmap_to_bool(mbm, n) if mbm is not None else None)
+
+    def flush_requests(self, cols: "RequestColumns", sigs=None, key_idx=None, assigned_seqs=None,
+                       digests: bool = True):
+        """pbftv_flush_requests: (digests | None, sig_ok | None, consensus digests | None)."""
+        n = cols.n
+        S, K, sbm = _sig_inputs(n, sigs, key_idx, "flush_requests")
+        out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
+        aseq = out_c = None
+        if assigned_seqs is not None:
+            aseq = np.ascontiguousarray(assigned_seqs, np.int64)
+            if aseq.shape != (n,):
+                raise ValueError("flush_requests: assigned_seqs must be (n,)")
+            out_c = np.zeros((max(n, 1), 32), np.uint8)
+        _check(self._L.pbftv_flush_requests(self._h, n, *cols.args(), _ptr(S), _ptr(K), _ptr(aseq), _ptr(out_d),
+                                            _ptr(sbm), _ptr(out_c)))
+        return (out_d[:n] if out_d is not None else None, bitmap_to_bool(sbm, n) if sbm is not None else None,
+                out_c[:n] if out_c is not None else None)
+
+    def flush_replies(self, cols: "ReplyColumns", sigs=None, key_idx=None, digests: bool = True):
+        """pbftv_flush_replies: (digests | None, sig_ok | None)."""
+        n = cols.n
+        S, K, sbm = _sig_inputs(n, sigs, key_idx, "flush_replies")
+        out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
+        _check(self._L.pbftv_flush_replies(self._h, n, *cols.args(), _ptr(S), _ptr(K), _ptr(out_d), _ptr(sbm)))
+        return (out_d[:n] if out_d is not None else None, bitmap_to_bool(sbm, n) if sbm is not None else None)
+
+    def flush_preprepares(self, cols: "PrePrepareColumns", sigs=None, key_idx=None, states=None, state_idx=None,
+                          digests: bool = True, req_digests: bool = False):
+        """pbftv_flush_preprepares: (digests | None, request digests | None, sig_ok | None, msg_ok | None).
+        states: (view_ids int64[k], last_seqs int64[k])."""
+        n = cols.n
+        S, K, sbm = _sig_inputs(n, sigs, key_idx, "flush_preprepares")
+        out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
+        out_r = np.zeros((max(n, 1), 32), np.uint8) if req_digests else None
+        k, sv, sl, si, mbm = 0, None, None, None, None
+        if states is not None:
+            k, sv, sl, _, si = _states(n, states, state_idx, "flush_preprepares", False)
+            mbm = np.zeros((n + 7) // 8 + 1, np.uint8)
+        _check(self._L.pbftv_flush_preprepares(self._h, n, *cols.args(), _ptr(S), _ptr(K), k, _ptr(sv), _ptr(sl),
+                                               _ptr(si), _ptr(out_d), _ptr(out_r), _ptr(sbm), _ptr(mbm)))
+        return (out_d[:n] if out_d is not None else None, out_r[:n] if out_r is not None else None,
+                bitmap_to_bool(sbm, n) if sbm is not None else None,
                 bitmap_to_bool(mbm, n) if mbm is not None else None)
 
     # ---- ecdsa

@@ -176,3 +176,128 @@ def test_flush_votes_fixture_signatures(ver, ecdsa_fixtures, path):
     votes = [(0, i, b"%064x" % i, b"node", 0) for i in range(n)]
     _, ok, _ = ver.flush_votes(VoteColumns(votes), sigs, kidx, digests=False)
     assert not ok.any()
+
+
+def _keys(oracle_lib, rng, n_keys):
+    privs, keys = [], np.zeros((n_keys, 64), np.uint8)
+    for k in range(n_keys):
+        d = int.from_bytes(rng.bytes(32), "big") % (N_ORDER - 1) + 1
+        privs.append(d.to_bytes(32, "big"))
+        assert oracle_lib.oracle_p256_pubkey(privs[-1], keys[k].ctypes.data) == 1
+    return privs, keys
+
+
+def _signed(oracle_lib, rng, preimages, privs):
+    """Sign each preimage with a random key; corrupt some (flipped r, wrong key).
+    Returns (sigs n x 64, key_idx, hashes n x 32)."""
+    n_keys = len(privs)
+    sigs, kidx, hs = [], [], []
+    for pre in preimages:
+        h = hashlib.sha256(pre).digest()
+        key = int(rng.integers(0, n_keys))
+        sig = _sign(oracle_lib, h, privs[key], rng)
+        c = int(rng.integers(0, 6))
+        if c == 0:
+            sig = bytes([sig[0] ^ 1]) + sig[1:]
+        elif c == 1:
+            key = (key + 1) % n_keys
+        sigs.append(sig)
+        kidx.append(key)
+        hs.append(h)
+    n = len(preimages)
+    return (np.frombuffer(b"".join(sigs), np.uint8).reshape(n, 64).copy(), np.array(kidx, np.uint32),
+            np.frombuffer(b"".join(hs), np.uint8).reshape(n, 32).copy())
+
+
+def _oracle_bits(oracle_lib, H, S, K, keys):
+    n = len(K)
+    want = np.zeros((n + 7) // 8 + 1, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(H.ctypes.data, S.ctypes.data, K.ctypes.data, n, keys.ctypes.data,
+                                              len(keys), want.ctypes.data, 8)
+    return np.unpackbits(want, bitorder="little")[:n].astype(bool).tolist()
+
+
+@pytest.mark.parametrize("n", [3, 67, 700])
+def test_flush_requests_vs_oracle(ver, oracle_lib, path, n):
+    """Client-signed requests (sequenceID as sent) + StartConsensus digests with
+    the assigned sequence IDs, one round trip (pbft_impl.go:67-73)."""
+    from simple_pbft_amd.pbftv import RequestColumns
+    rng = np.random.default_rng(2000 + n)
+    privs, keys = _keys(oracle_lib, rng, 4)
+    assert ver.register_keys(keys).all()
+    reqs = [(rand_int(rng), rand_str(rng), rand_str(rng, 30), 0 if rng.integers(0, 4) else rand_int(rng))
+            for _ in range(n)]
+    pre = [gojson.request(*r) for r in reqs]
+    S, K, H = _signed(oracle_lib, rng, pre, privs)
+    assigned = np.array([rand_int(rng) for _ in range(n)], np.int64)
+    dg, ok, cons = ver.flush_requests(RequestColumns(reqs), S, K, assigned)
+    assert hexes(dg) == [sha(p) for p in pre]
+    assert ok.tolist() == _oracle_bits(oracle_lib, H, S, K, keys)
+    assert hexes(cons) == [sha(gojson.request(r[0], r[1], r[2], int(a))) for r, a in zip(reqs, assigned)]
+    if n >= 67:
+        assert ok.any() and not ok.all()
+    d2, s2, c2 = ver.flush_requests(RequestColumns(reqs), S, K, digests=False)
+    assert d2 is None and c2 is None and s2.tolist() == ok.tolist()
+
+
+@pytest.mark.parametrize("n", [3, 67, 700])
+def test_flush_replies_vs_oracle(ver, oracle_lib, path, n):
+    from simple_pbft_amd.pbftv import ReplyColumns
+    rng = np.random.default_rng(3000 + n)
+    privs, keys = _keys(oracle_lib, rng, 4)
+    assert ver.register_keys(keys).all()
+    reps = [(rand_int(rng), rand_int(rng), rand_str(rng), b"node%d" % int(rng.integers(0, 4)),
+             [b"Executed", rand_str(rng, 40)][int(rng.integers(0, 2))]) for _ in range(n)]
+    pre = [gojson.reply(*r) for r in reps]
+    S, K, H = _signed(oracle_lib, rng, pre, privs)
+    dg, ok = ver.flush_replies(ReplyColumns(reps), S, K)
+    assert hexes(dg) == [sha(p) for p in pre]
+    assert ok.tolist() == _oracle_bits(oracle_lib, H, S, K, keys)
+    if n >= 67:
+        assert ok.any() and not ok.all()
+
+
+@pytest.mark.parametrize("n", [3, 67, 700])
+def test_flush_preprepares_vs_oracle(ver, oracle_lib, path, n):
+    """Primary-signed pre-prepares: signature over Go-JSON(PrePrepareMsg), and
+    State.PrePrepare's verifyMsg with the embedded request as the state's ReqMsg
+    (nil request -> digest of "null"), against several states."""
+    from simple_pbft_amd.pbftv import PrePrepareColumns
+    rng = np.random.default_rng(4000 + n)
+    privs, keys = _keys(oracle_lib, rng, 3)
+    assert ver.register_keys(keys).all()
+    k_states = 5
+    s_view = np.array([0, 0, 3, 0, 7], np.int64)
+    s_last = np.array([-1, 50, -1, 1000, 20], np.int64)
+    pps, sidx = [], []
+    for i in range(n):
+        st = int(rng.integers(0, k_states + 1))
+        req = None if rng.integers(0, 6) == 0 else (rand_int(rng), rand_str(rng), rand_str(rng, 20),
+                                                    int(rng.integers(0, 300)))
+        rd = hashlib.sha256(gojson.request_or_null(req)).hexdigest().encode()
+        kind = int(rng.integers(0, 7))
+        dg = [rd, rd, rd, rd.upper(), rd[:-1], rand_str(rng, 64), rd + b"1"][kind]
+        view = int(s_view[min(st, k_states - 1)]) + (1 if rng.integers(0, 8) == 0 else 0)
+        seq = req[3] if req is not None and rng.integers(0, 2) else int(rng.integers(0, 2000))
+        pps.append((view, seq, dg, req))
+        sidx.append(st)
+    pre = [gojson.preprepare(*p) for p in pps]
+    S, K, H = _signed(oracle_lib, rng, pre, privs)
+    dg, rdg, ok, mok = ver.flush_preprepares(PrePrepareColumns(pps), S, K, (s_view, s_last), np.array(sidx, np.uint32),
+                                             req_digests=True)
+    assert hexes(dg) == [sha(p) for p in pre]
+    assert hexes(rdg) == [sha(gojson.request_or_null(p[3])) for p in pps]
+    assert ok.tolist() == _oracle_bits(oracle_lib, H, S, K, keys)
+    want_msg = []
+    for (view, seq, d, req), st in zip(pps, sidx):
+        if st >= k_states:
+            want_msg.append(False)
+            continue
+        qd = hashlib.sha256(gojson.request_or_null(req)).digest()
+        want_msg.append(oracle_lib.oracle_verify_msg(int(s_view[st]), int(s_last[st]), qd, view, seq, d,
+                                                     len(d)) == 1)
+    assert mok.tolist() == want_msg
+    if n >= 67:
+        assert ok.any() and not ok.all() and any(want_msg) and not all(want_msg)
+    # digests only (the pbftv_digest_preprepare_batch body) agree
+    assert hexes(ver.digest_preprepare_batch(pps)) == hexes(dg)

@@ -51,6 +51,51 @@ def test_vote_signed_known_answer(pb):
         assert got == b'{"viewID":0,"sequenceID":1,"digest":"d","nodeID":"MS","msgType":1,"signature":' + enc + b"}"
 
 
+def _rand_bytes(rng, lo=0, hi=40):
+    return bytes(rng.randrange(256) for _ in range(rng.randrange(lo, hi)))
+
+
+def _rand_sig(rng):
+    return None if rng.random() < 0.15 else _rand_bytes(rng, 0, 80)
+
+
+def test_other_signed_messages_match_restatement(pb):
+    """Signed RequestMsg / ReplyMsg / PrePrepareMsg wire forms
+    against oracle/gojson.py, and the signing preimage is the unsigned encoding
+    (a strict prefix of the wire form)."""
+    rng = random.Random(0x5349474E)
+    for _ in range(200):
+        ts, seq = rng.randrange(-(1 << 62), 1 << 62), rng.randrange(-(1 << 62), 1 << 62)
+        cid, op, res = _rand_bytes(rng), _rand_bytes(rng), _rand_bytes(rng)
+        nid = rng.choice([b"Apple", b"MS", b"<n\x00d\xe2\x80\xa8>"])
+        sig, rsig = _rand_sig(rng), _rand_sig(rng)
+        want = gojson.request_signed(ts, cid, op, seq, sig)
+        assert pb.gojson_request_signed(ts, cid, op, seq, sig) == want
+        assert want.startswith(pb.gojson_request(ts, cid, op, seq)[:-1])
+        view = rng.randrange(-5, 1 << 40)
+        want = gojson.reply_signed(view, ts, cid, nid, res, sig)
+        assert pb.gojson_reply_signed(view, ts, cid, nid, res, sig) == want
+        assert want.startswith(pb.gojson_reply(view, ts, cid, nid, res)[:-1])
+        req = None if rng.random() < 0.2 else (ts, cid, op, seq)
+        dg = _rand_bytes(rng, 0, 70)
+        want = gojson.preprepare_signed(view, seq, dg, req, rsig, sig)
+        assert pb.gojson_preprepare_signed(view, seq, dg, req, rsig, sig) == want
+        # the primary's preimage embeds the unsigned request
+        assert pb.gojson_preprepare(view, seq, dg, req) == gojson.preprepare(view, seq, dg, req)
+
+
+def test_signed_messages_known_answer(pb):
+    assert pb.gojson_request_signed(1668519246, b"client1", b"printf", 0, b"foo") == (
+        b'{"timestamp":1668519246,"clientID":"client1","operation":"printf","sequenceID":0,"signature":"Zm9v"}')
+    assert pb.gojson_reply_signed(0, 5, b"c", b"MS", b"Executed", None) == (
+        b'{"viewID":0,"timestamp":5,"clientID":"c","nodeID":"MS","result":"Executed","signature":null}')
+    assert pb.gojson_preprepare_signed(0, 7, b"ab", (1, b"c", b"o", 7), b"f", b"fo") == (
+        b'{"viewID":0,"sequenceID":7,"digest":"ab","requestMsg":{"timestamp":1,"clientID":"c","operation":"o",'
+        b'"sequenceID":7,"signature":"Zg=="},"signature":"Zm8="}')
+    assert pb.gojson_preprepare_signed(0, 7, b"ab", None, b"f", b"") == (
+        b'{"viewID":0,"sequenceID":7,"digest":"ab","requestMsg":null,"signature":""}')
+
+
 def _malformed():
     good = der_ref.encode(0x1234, N - 1)
     body = good[2:]

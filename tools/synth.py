@@ -184,41 +184,62 @@ NODES = [b"MainNode", b"ReplicaNode1", b"ReplicaNode2", b"ReplicaNode3"]  # pbft
 VIEW = 10000000000                                                         # node.go:55
 
 
-def config1_cluster(n_req: int = 1000, seed: int = 0x50424654):
+CLIENT_KEY = 4  # key index of the (one) client process in config 1
+
+
+def config1_cluster(n_req: int = 1000, seed: int = 0x50424654) -> dict:
     """the reference's 4-node message pattern for n_req
-    requests.  Per request: 3 replica prepares each verified by 3 peers (9), 4
-    commits each verified by 3 peers (12), 4 replies verified by the primary (4)
-    = 25 signature checks over 11 distinct signed messages; every prepare/commit
-    also re-checks the request digest (reference: 20 digest recomputes)."""
+    requests, every message signed.  Per request: the client's
+    request verified by the primary (1), the primary's pre-prepare verified by
+    3 replicas (3), 3 replica prepares each verified by 3 peers (9), 4 commits
+    each verified by 3 peers (12), 4 replies verified by the client (4) = 29
+    signature checks over 13 distinct signed messages.  Keys: the 4 nodes
+    (NODES order) and the client (CLIENT_KEY).  The client signs its request
+    with sequenceID 0 (as sent); StartConsensus assigns the sequence ID
+    (pbft_impl.go:57-67) before the request digest is taken."""
     sys_path_fix()
-    from simple_pbft_amd import pbftv as gojson  # host-only Go-JSON encoder of the product (no GPU)
-    gojson.request, gojson.vote, gojson.reply = gojson.gojson_request, gojson.gojson_vote, gojson.gojson_reply
-    s = Signer(4, seed)
-    reqs, votes, vote_sig, replies, reply_sig = [], [], [], [], []
+    from simple_pbft_amd import pbftv as gj  # host-only Go-JSON encoder of the product (no GPU)
+    s = Signer(5, seed)
+    sent, assigned, req_sig = [], [], []
+    pps, pp_sig = [], []
+    votes, vote_sig, replies, reply_sig = [], [], [], []
     checks = []  # (kind, index, receiver)
     for i in range(n_req):
-        req = (1668519246 + i, b"client%d" % i, b"printf", 1668519247222762700 + 1000 * i)
-        reqs.append(req)
-        d = hashlib.sha256(gojson.request(*req)).hexdigest().encode()
+        req0 = (1668519246 + i, b"client%d" % i, b"printf", 0)
+        sent.append(req0)
+        req_sig.append(s.sign(hashlib.sha256(gj.gojson_request(*req0)).digest(), CLIENT_KEY))
+        seq = 1668519247222762700 + 1000 * i
+        assigned.append(seq)
+        req = req0[:3] + (seq,)
+        checks.append(("request", i, 0))
+        d = hashlib.sha256(gj.gojson_request(*req)).hexdigest().encode()
+        pp = (VIEW, seq, d, req)
+        pps.append(pp)
+        pp_sig.append(s.sign(hashlib.sha256(gj.gojson_preprepare(*pp)).digest(), 0))
+        checks += [("preprepare", len(pps) - 1, r) for r in (1, 2, 3)]
         for sender in (1, 2, 3):                       # prepares from the replicas
-            v = (VIEW, req[3], d, NODES[sender], 0)
+            v = (VIEW, seq, d, NODES[sender], 0)
             votes.append(v)
-            vote_sig.append(s.sign(hashlib.sha256(gojson.vote(*v)).digest(), sender))
+            vote_sig.append(s.sign(hashlib.sha256(gj.gojson_vote(*v)).digest(), sender))
             checks += [("vote", len(votes) - 1, r) for r in range(4) if r != sender]
         for sender in range(4):                        # commits from every node
-            v = (VIEW, req[3], d, NODES[sender], 1)
+            v = (VIEW, seq, d, NODES[sender], 1)
             votes.append(v)
-            vote_sig.append(s.sign(hashlib.sha256(gojson.vote(*v)).digest(), sender))
+            vote_sig.append(s.sign(hashlib.sha256(gj.gojson_vote(*v)).digest(), sender))
             checks += [("vote", len(votes) - 1, r) for r in range(4) if r != sender]
-        for sender in range(4):                        # replies to the primary
+        for sender in range(4):                        # replies to the client
             rp = (VIEW, req[0], req[1], NODES[sender], b"Executed")
             replies.append(rp)
-            reply_sig.append(s.sign(hashlib.sha256(gojson.reply(*rp)).digest(), sender))
-            checks.append(("reply", len(replies) - 1, 0))
+            reply_sig.append(s.sign(hashlib.sha256(gj.gojson_reply(*rp)).digest(), sender))
+            checks.append(("reply", len(replies) - 1, 4))
     pub = s.pub.copy()
     s.close()
-    return pub, reqs, votes, np.frombuffer(b"".join(vote_sig), np.uint8).reshape(-1, 64), replies, \
-        np.frombuffer(b"".join(reply_sig), np.uint8).reshape(-1, 64), checks
+
+    def rows(sigs):
+        return np.frombuffer(b"".join(sigs), np.uint8).reshape(-1, 64)
+    return {"pub": pub, "requests": sent, "request_sigs": rows(req_sig), "assigned_seqs": np.array(assigned, np.int64),
+            "preprepares": pps, "preprepare_sigs": rows(pp_sig), "votes": votes, "vote_sigs": rows(vote_sig),
+            "replies": replies, "reply_sigs": rows(reply_sig), "checks": checks}
 
 
 def certs(n_keys: int, per_cert: int, n_certs: int, seed: int):
