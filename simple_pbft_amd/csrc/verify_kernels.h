@@ -375,9 +375,11 @@ __device__ __forceinline__ void quad_bcast(fe& d, const fe& s) {
 __device__ __forceinline__ uint32_t mask_of(bool c) { return 0u - (uint32_t)c; }
 
 __device__ __forceinline__ void quad_sel(fe& d, int role, const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
-  const uint32_t m0 = mask_of(role == 0), m1 = mask_of(role == 1), m2 = mask_of(role == 2), m3 = mask_of(role == 3);
-  PBFTV_UNROLL for (int l = 0; l < 9; ++l)
-    d.v[l] = (a0.v[l] & m0) | (a1.v[l] & m1) | (a2.v[l] & m2) | (a3.v[l] & m3);
+  const bool b0 = (role & 1) != 0, b1 = (role & 2) != 0;  // three v_cndmask per limb
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+    const uint32_t lo = b0 ? a1.v[l] : a0.v[l], hi = b0 ? a3.v[l] : a2.v[l];
+    d.v[l] = b1 ? hi : lo;
+  }
 }
 
 // d = c0 ? a : c1 ? b : c   (masks, see above)
@@ -519,25 +521,192 @@ __device__ __forceinline__ void wave_sum_quads(xyzz_s& P, bool& inf, bool& exc, 
   }
 }
 
-// ecdsa_scalars with the inversion fed the plain s (no Montgomery round trip
-// in front of it): w = s^-1 -> w R -> u1 = e w, u2 = r w (two independent
-// products) -- one dependent Montgomery product fewer on the latency path.
-__device__ __forceinline__ void ecdsa_scalars_plain_inv(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
-                                                        uint32_t u1[8], uint32_t u2[8]) {
-  uint32_t iw[8];
-  inv_mod_n_words(iw, s);  // 0 < s < n checked by sig_ok
-  fe inv, r2n, w, ev, rv, t1, t2;
-  fe_from_words(inv, iw);
-  fe_set(r2n, kR2N);
-  fn_mul(w, inv, r2n);     // s^-1 R
+// ---- latency-path scalars: the inversion spread over the wave --------------
+// Bernstein-Yang safegcd (safegcd.h) with the work split by kind: the 30
+// divsteps of a batch are a short serial chain on the low 30 bits of (f, g)
+// and run on the SCALAR unit (uniform operands from v_readlane), while the
+// 2x2 matrix update of the 270-bit (f, g) and (d, e) is one LANE PER LIMB:
+//   lanes 0..8   limb L of f (A) and g (B)       (row 0 of the DPP rows)
+//   lanes 16..24 limb L of d (A) and e (B) mod n (row 1)
+// Limbs are 30-bit signed, kept centered (|limb| <= 2^29 + 2; the top limb is
+// free), so u A + v B + md n_L stays below 2^60 in magnitude and the shifted
+// limbs fit int32; the division by 2^30 moves each limb's low part one lane
+// down (DPP row_shl:1) and a centered carry pass moves carries one lane up
+// (row_shr:1).  md is the centered multiple of n that makes (d, e)'s low limb
+// vanish; without the sign-dependent range keeping of update_de30, |d| grows by
+// at most n/2 per batch (< 13.5 n after 25 batches; tests/test_algo_cpu.py
+// emulates the scheme and checks every bound).  e starts at R mod n, so the
+// result is R s^-1 (Montgomery form for the u1 / u2 products, no extra one).
+__device__ __forceinline__ int32_t lane_from_next(int32_t x) {  // lane j <- lane j + 1 of its row (0 past the row)
+  return __builtin_amdgcn_update_dpp(0, x, 0x101, 0xF, 0xF, true);
+}
+__device__ __forceinline__ int32_t lane_from_prev(int32_t x) {  // lane j <- lane j - 1 of its row (0 before it)
+  return __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ int32_t center30(uint32_t x) { return (int32_t)(x << 2) >> 2; }
+
+// limb re-centering: carry (x + 2^29) >> 30 one lane up (not out of the top limb)
+__device__ __forceinline__ int32_t limbs_center(int32_t x, bool top) {
+  const int32_t c = top ? 0 : (x + (1 << 29)) >> 30;
+  return x - (int32_t)((uint32_t)c << 30) + lane_from_prev(c);
+}
+
+// (sum over lanes) / 2^30 of a 64-bit column whose low 30 bits vanish
+__device__ __forceinline__ int32_t limbs_shift30(int64_t p) {
+  const uint32_t lo32 = (uint32_t)p;
+  const int32_t lo = center30(lo32);
+  const int32_t hi = (int32_t)__builtin_amdgcn_alignbit((uint32_t)((uint64_t)p >> 32), lo32, 30) +
+                     (int32_t)((lo32 >> 29) & 1u);  // floor(p / 2^30) + (lo < 0)
+  return hi + lane_from_next(lo);
+}
+
+// per-lane limb L (< 9) of a uniform 9-limb value
+__device__ __forceinline__ uint32_t lane_limb(const uint32_t v[9], int L) {
+  uint32_t r = 0;
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) r = L == k ? v[k] : r;
+  return r;
+}
+
+// D = R x^-1 mod n + k n for some k >= 0 (D < 2^261, 29-bit limbs, uniform),
+// for 0 < x < n (uniform LE words).  Every lane of the wave must call it.
+__device__ __forceinline__ void inv_mod_n_wave(fe& D, const uint32_t x[8]) {
+  const int lane = (int)(threadIdx.x & 63u), L = lane & 15, row = lane >> 4;
+  const bool act = L < 9 && row < 2, top = L == 8;
+  s30 xs, rn;
+  words_to_s30(xs, x);
+  {
+    uint32_t rw[8];  // R mod n = 2^261 mod n as words: from kOneN (R mod n in 29-bit limbs)
+    fe one;
+    fe_set(one, kOneN);
+    fe_to_words(rw, one);
+    words_to_s30(rn, rw);
+  }
+  const uint32_t nl = act && row == 1 ? lane_limb(kN30, L) : 0u;
+  int32_t A = act && row == 0 ? (int32_t)lane_limb(kN30, L) : 0;                         // f = n, d = 0
+  const uint32_t xl = lane_limb(reinterpret_cast<const uint32_t*>(xs.v), L);
+  const uint32_t rl = lane_limb(reinterpret_cast<const uint32_t*>(rn.v), L);
+  int32_t B = act ? (int32_t)(row == 0 ? xl : rl) : 0;  // g = x, e = R mod n
+  A = limbs_center(A, top);
+  B = limbs_center(B, top);
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int it = 0; it < 25; ++it) {
+    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(B, 0);
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane(A, 16), e0 = (uint32_t)__builtin_amdgcn_readlane(B, 16);
+    trans30 t;
+    eta = divsteps30_var(eta, f0, g0, t);
+    const int32_t md = center30(0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * kNInv30);
+    const int32_t me = center30(0u - ((uint32_t)t.q * d0 + (uint32_t)t.r * e0) * kNInv30);
+    const int64_t P = (int64_t)t.u * A + (int64_t)t.v * B + (int64_t)md * (int32_t)nl;
+    const int64_t Q = (int64_t)t.q * A + (int64_t)t.r * B + (int64_t)me * (int32_t)nl;
+    A = limbs_center(limbs_shift30(P), top);
+    B = limbs_center(limbs_shift30(Q), top);
+    if (__ballot(row == 0 && B != 0) == 0) break;  // g == 0: f = +-1, d = +-R x^-1
+  }
+  uint32_t fl0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), fl1 = (uint32_t)__builtin_amdgcn_readlane(A, 1);
+  const bool pos = fl0 + (fl1 << 30) == 1u;  // f = +-1: its value mod 2^32
+  // D = +-d + 16 n > 0 (|d| < 13.5 n), normalised 30-bit limbs, then 29-bit limbs
+  uint32_t w30[9];
+  int64_t c = 0;
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) {
+    const int32_t dk = __builtin_amdgcn_readlane(A, 16 + k);
+    c += (int64_t)(pos ? dk : -dk) + 16 * (int64_t)kN30[k];
+    if (k < 8) {
+      w30[k] = (uint32_t)c & kM30;
+      c >>= 30;
+    } else {
+      w30[k] = (uint32_t)c;
+    }
+  }
+  PBFTV_UNROLL for (int j = 0; j < 9; ++j) {
+    const int bit = 29 * j, li = bit / 30, sh = bit % 30;
+    uint32_t v = w30[li] >> sh;
+    if (li + 1 < 9) v |= w30[li + 1] << (30 - sh);
+    D.v[j] = v & kMask29;
+  }
+}
+
+// a b 2^-261 mod m with a per-lane modulus m (29-bit limbs) and mp = -m^-1 mod
+// 2^29: one step of the latency path runs mod-n and mod-p products side by
+// side on different lanes.  Inputs limbs < 2^29, a < 2^257, b < 2^261;
+// output < a b / 2^261 + m, limbs < 2^29.
+__device__ __forceinline__ void fmont_lane(fe& r, const fe& a, const fe& b, const fe& m, uint32_t mp) {
+  uint64_t t[18];
+  PBFTV_UNROLL for (int k = 0; k < 18; ++k) t[k] = 0;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * b.v[j];
+    const uint32_t q = ((uint32_t)t[i] * mp) & kMask29;
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)q * m.v[j];
+    t[i + 1] += t[i] >> 29;
+  }
+  PBFTV_UNROLL for (int j = 9; j < 16; ++j) {
+    r.v[j - 9] = (uint32_t)t[j] & kMask29;
+    t[j + 1] += t[j] >> 29;
+  }
+  r.v[7] = (uint32_t)t[16] & kMask29;
+  r.v[8] = (uint32_t)(t[16] >> 29);
+}
+
+__device__ __forceinline__ void fe_readlane(fe& d, const fe& s, int lane) {
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) d.v[l] = (uint32_t)__builtin_amdgcn_readlane((int)s.v[l], lane);
+}
+
+// Go's scalars for the latency path (0 < r, s < n checked by the caller), all
+// uniform: u1 = e s^-1, u2 = r s^-1 mod n (LE words), and r, r + n in
+// Montgomery form mod p for the final check (rn_ok: r + n < p).  One
+// inversion (inv_mod_n_wave), then ONE product step: lanes 4k..4k+3 compute
+// e D, r D (mod n) and r R^2, (r + n) R^2 (mod p) at once.
+__device__ __forceinline__ void wave_scalars(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
+                                             uint32_t u1[8], uint32_t u2[8], fe& rm, fe& rnm, bool& rn_ok) {
+  fe D;
+  inv_mod_n_wave(D, s);
+  uint32_t rn[8];
+  uint64_t cy = 0;
+  PBFTV_UNROLL for (int i = 0; i < 8; ++i) {
+    cy += (uint64_t)r[i] + kN32[i];
+    rn[i] = (uint32_t)cy;
+    cy >>= 32;
+  }
+  rn_ok = words_lt(r, kPMinusN32);  // r + n < p
+  const int role = (int)(threadIdx.x & 3u);
+  fe ev, rv, rnv, a, b, m, r2p, nmod, pmod, prod;
   fe_from_words(ev, e);
   fe_from_words(rv, r);
-  fn_mul(t1, ev, w);       // e s^-1 (e < 2^256 < 2n)
-  fn_mul(t2, rv, w);
-  fn_canon(t1, t1);
-  fn_canon(t2, t2);
-  fe_to_words(u1, t1);
-  fe_to_words(u2, t2);
+  fe_from_words(rnv, rn);
+  fe_set(r2p, kR2P);
+  fe_set(nmod, kN);
+  fe_set(pmod, kP);
+  const bool modn = role < 2;
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+    a.v[l] = role == 0 ? ev.v[l] : (role == 3 ? rnv.v[l] : rv.v[l]);
+    b.v[l] = modn ? D.v[l] : r2p.v[l];
+    m.v[l] = modn ? nmod.v[l] : pmod.v[l];
+  }
+  fmont_lane(prod, a, b, m, modn ? kNPrime : 1u);  // p = -1 mod 2^29: -p^-1 = 1
+  fn_canon(a, prod);  // lanes 0, 1: < 2^256 + n  ->  [0, n) in two steps
+  fn_canon(a, a);
+  uint32_t w[8];
+  fe_to_words(w, a);
+  PBFTV_UNROLL for (int k = 0; k < 8; ++k) {
+    u1[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 0);
+    u2[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 1);
+  }
+  fe_readlane(rm, prod, 2);
+  fe_readlane(rnm, prod, 3);
+}
+
+// x(P) == r or r + n (mod n) for the all-reduced XYZZ sum: lanes 0 and 1 test
+// X == r ZZ and X == (r + n) ZZ with one product step.
+__device__ __forceinline__ bool wave_check(const xyzz_s& P, bool finite, const fe& rm, const fe& rnm, bool rn_ok) {
+  const int role = (int)(threadIdx.x & 1u);
+  fe a, lhs, d;
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) a.v[l] = role ? rnm.v[l] : rm.v[l];
+  fs_mul(lhs, a, P.zz);
+  fs_sub(d, lhs, P.x);
+  const bool z = fs_is_zero(d);
+  const unsigned long long bz = __ballot(z);
+  return finite && ((bz & 1ull) != 0 || (rn_ok && (bz & 2ull) != 0));
 }
 
 template <int WG, int WQ>
@@ -556,8 +725,15 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
   uint32_t r[8], s[8], e[8];
   load_be256(hashes + 32 * i, e);  // issued with sig_ok's loads: one round trip to the (host) inputs
   if (sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s)) {  // wave-uniform branch
+    PBFTV_UNROLL for (int k = 0; k < 8; ++k) {  // one copy per wave (the loads are per lane)
+      e[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[k]);
+      r[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[k]);
+      s[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[k]);
+    }
     uint32_t u1[8], u2[8];
-    ecdsa_scalars_plain_inv(e, r, s, u1, u2);
+    fe rm, rnm;
+    bool rn_ok;
+    wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
     const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
     bool inf;
     bool exc = true;
@@ -565,7 +741,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
       xyzz_s P;
       wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
       exc = __any(exc);
-      if (!exc) ok = ecdsa_check(P, !inf, r);
+      if (!exc) ok = wave_check(P, !inf, rm, rnm, rn_ok);
     }
     if (exc) {  // windows outnumber the quads, or a doubling somewhere: exact lane-per-window rerun
       jac P;

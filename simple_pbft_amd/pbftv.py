@@ -736,6 +736,27 @@ class Verifier:
         _check(self._L.pbftv_sha256_batch_dev(self._h, dev, d_data, d_offsets, d_lengths, d_order, n, d_digests,
                                               d_expected, d_bitmap, stream))
 
+    def qc_verify_prepared(self, hashes, sig_rs, key_idx, quorum: int):
+        """A zero-argument callable running pbftv_qc_verify on fixed inputs with every
+        argument marshalled once (the per-call cost is then the library's plus one
+        ctypes call, as for a cgo caller); returns (accepted, quorum reached)."""
+        hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)
+        sig_rs = np.ascontiguousarray(sig_rs, np.uint8).reshape(-1, 64)
+        key_idx = np.ascontiguousarray(key_idx, np.uint32)
+        n = hashes.shape[0]
+        bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+        acc, ok = ctypes.c_uint64(), ctypes.c_int()
+        fn = self._L.pbftv_qc_verify
+        args = (self._h, _vp(hashes.ctypes.data), _vp(sig_rs.ctypes.data), _vp(key_idx.ctypes.data),
+                ctypes.c_uint64(n), ctypes.c_uint32(quorum), _vp(bm.ctypes.data), ctypes.byref(acc),
+                ctypes.byref(ok))
+
+        def call():
+            _check(fn(*args))
+            return acc.value, bool(ok.value)
+        call.keep = (hashes, sig_rs, key_idx, bm)  # the buffers live as long as the callable
+        return call
+
     def qc_verify(self, hashes, sig_rs, key_idx, quorum: int):
         hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)
         sig_rs = np.ascontiguousarray(sig_rs, np.uint8).reshape(-1, 64)

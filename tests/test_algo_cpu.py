@@ -426,3 +426,110 @@ def test_xyzz_madd_s_chain_values_and_bounds(H):
         a2 = A(*acc)
         H.h_xyzz_madd_s(a2, Pt(*limbs(mont(x)), *limbs(mont(y))))
         assert sval(a2[18:27]) % P == 0 and sval(a2[27:36]) % P == 0
+
+
+# ---- lane-parallel safegcd of the latency path (verify_kernels.h inv_mod_n_wave) ----
+# A restatement of the kernel's scheme with exact integers: one list entry per
+# lane-limb, 30-bit signed limbs re-centered after every batch, divsteps on the
+# low limbs only, centered md / me, no sign-dependent range keeping, e = R mod n
+# at the start.  Checks what the kernel's int32 / int64 arithmetic relies on.
+_N = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+_M30 = (1 << 30) - 1
+
+
+def _s32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >> 31 else x
+
+
+def _i32(x):
+    assert -(1 << 31) <= x < (1 << 31)
+    return x
+
+
+def _divsteps30_var(eta, f, g):
+    """safegcd.h divsteps30_var on 32-bit words."""
+    u, v, q, r, i = 1, 0, 0, 1, 30
+    f &= 0xFFFFFFFF
+    g &= 0xFFFFFFFF
+    while True:
+        gg = (g | (0xFFFFFFFF << i)) & 0xFFFFFFFF
+        z = (gg & -gg).bit_length() - 1
+        g >>= z
+        u = (u << z) & 0xFFFFFFFF
+        v = (v << z) & 0xFFFFFFFF
+        eta -= z
+        i -= z
+        if i == 0:
+            return eta, _s32(u), _s32(v), _s32(q), _s32(r)
+        if eta < 0:
+            eta = -eta
+            f, g, u, q, v, r = g, -f & 0xFFFFFFFF, q, -u & 0xFFFFFFFF, r, -v & 0xFFFFFFFF
+        m = (0xFFFFFFFF >> (32 - min(eta + 1, i))) & 63
+        w = (f * g * ((f * f - 2) & 0xFFFFFFFF)) & m
+        g, q, r = (g + f * w) & 0xFFFFFFFF, (q + u * w) & 0xFFFFFFFF, (r + v * w) & 0xFFFFFFFF
+
+
+def _center(limbs):
+    cs = [((x + (1 << 29)) >> 30) if L < 8 else 0 for L, x in enumerate(limbs)]
+    return [_i32(x - (c << 30) + (cs[L - 1] if L else 0)) for L, (x, c) in enumerate(zip(limbs, cs))]
+
+
+def _shift30(cols):
+    for p in cols:
+        assert abs(p) < (1 << 61)  # int64 with room: |u A + v B + md n_L| < 2^60.x
+    lo = [((p & _M30) ^ (1 << 29)) - (1 << 29) for p in cols]
+    assert lo[0] == 0  # the batch's matrix makes the low limb vanish
+    hi = [_i32((p - l) >> 30) for p, l in zip(cols, lo)]
+    return [_i32(hi[L] + (lo[L + 1] if L < 8 else 0)) for L in range(9)]
+
+
+def _limbs30(x):
+    return [(x >> (30 * L)) & _M30 for L in range(8)] + [x >> 240]
+
+
+def _value(limbs):
+    return sum(v << (30 * L) for L, v in enumerate(limbs))
+
+
+def _inv_wave(x):
+    n_l = _limbs30(_N)
+    f, g = _center(n_l), _center(_limbs30(x))
+    d, e = [0] * 9, _center(_limbs30((1 << 261) % _N))
+    eta, batches = -1, 0
+    for _ in range(25):
+        batches += 1
+        eta, u, v, q, r = _divsteps30_var(eta, f[0], g[0])
+        d0, e0 = d[0] & 0xFFFFFFFF, e[0] & 0xFFFFFFFF
+        md = _s32((-((u * d0 + v * e0) * 0x11FF43B1)) << 2) >> 2   # center30(0 - c nInv30)
+        me = _s32((-((q * d0 + r * e0) * 0x11FF43B1)) << 2) >> 2
+        f, g = (_center(_shift30([u * a + v * b for a, b in zip(f, g)])),
+                _center(_shift30([q * a + r * b for a, b in zip(f, g)])))
+        d, e = (_center(_shift30([u * a + v * b + md * nl for a, b, nl in zip(d, e, n_l)])),
+                _center(_shift30([q * a + r * b + me * nl for a, b, nl in zip(d, e, n_l)])))
+        for limbs in (f, g, d, e):
+            assert all(abs(t) <= (1 << 29) + 2 for t in limbs[:8])
+        assert abs(_value(d)) < 13.5 * _N and abs(_value(e)) < 13.5 * _N
+        if not any(g):
+            break
+    fv = _value(f)
+    assert fv in (1, -1)
+    pos = (f[0] + (f[1] << 30)) & 0xFFFFFFFF == 1  # the kernel's sign test
+    assert pos == (fv == 1)
+    D = (_value(d) if pos else -_value(d)) + 16 * _N
+    assert 0 < D < (1 << 261)
+    return D, batches
+
+
+def test_lane_parallel_safegcd_bounds_and_result():
+    import random
+    rng = random.Random(0x494E56)
+    xs = [1, 2, 3, _N - 1, _N - 2, 1 << 255, (1 << 256) % _N, 0x7FFFFFFF, 1 << 30, (1 << 30) - 1]
+    xs += [rng.randrange(1, _N) for _ in range(1500)]
+    xs += [rng.randrange(1, 1 << rng.randrange(1, 257)) % _N or 1 for _ in range(300)]
+    most = 0
+    for x in xs:
+        D, batches = _inv_wave(x)
+        assert D % _N == (1 << 261) * pow(x, -1, _N) % _N
+        most = max(most, batches)
+    assert most <= 25

@@ -35,7 +35,8 @@ def main():
     for n_keys, sigs in ((4, 3), (100, 67)):
         pub, H, S, K = synth.qc(n_keys, sigs, 5)
         ver.register_keys(pub)
-        r = {"qc_verify_us": p50(lambda: ver.qc_verify(H, S, K, quorum=sigs))}
+        r = {"qc_verify_us": p50(lambda: ver.qc_verify(H, S, K, quorum=sigs)),
+             "qc_verify_prepared_us": p50(ver.qc_verify_prepared(H, S, K, quorum=sigs))}
         dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
         db = ver.alloc(0, 64)
 

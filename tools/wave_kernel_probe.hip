@@ -1,10 +1,12 @@
 // wave_kernel_probe.hip -- stage timestamps of the one-wave-per-signature
-// latency kernel (k_ecdsa_wave's body, p256_kernels.hip, replicated with
-// wall_clock64() stamps): input loads, scalars (safegcd), quad comb, check.
-// Tables: 24-bit G and one 22-bit key table (Q = G), built with the product's
-// table kernels.  Measurement tool for DESIGN.md (not part of the product).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/wave_kernel_probe.hip -o tools/wave_kernel_probe
-#include "../simple_pbft_amd/csrc/p256_kernels.hip"
+// latency kernel (k_ecdsa_wave's body, verify_kernels.h, replicated with
+// wall_clock64() stamps): input loads, scalars (lane-parallel safegcd + one
+// product step), quad comb, check; plus the inversion alone.  Tables: the
+// n = 4 geometry (29-bit G, one 24-bit key table with Q = G), built with the
+// product's table kernels.  Measurement tool for DESIGN.md (not the product).
+//   make -C simple_pbft_amd && hipcc --offload-arch=gfx950 -O3 -std=c++17 -c tools/wave_kernel_probe.hip -o p.o \
+//   && hipcc --offload-arch=gfx950 p.o simple_pbft_amd/build/p256_*.o -o tools/wave_kernel_probe
+#include "../simple_pbft_amd/csrc/verify_kernels.h"
 
 #include <cstdio>
 #include <vector>
@@ -14,7 +16,7 @@ using namespace pbftv;
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
-constexpr int WG = 24, WQ = 22;
+constexpr int WG = 29, WQ = 24;
 
 __global__ void __launch_bounds__(64) probe(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
                                             const uint32_t* key_valid, const uint4* gtab, const uint4* qtabs,
@@ -26,11 +28,18 @@ __global__ void __launch_bounds__(64) probe(const uint8_t* hashes, const uint8_t
   load_be256(hashes + 32 * i, e);
   const bool okin = sig_ok(sigs, key_idx, key_valid, 1, i, r, s);
   uint32_t acc = okin;
-  for (int k = 0; k < 8; ++k) acc += e[k] ^ r[k] ^ s[k];
+  for (int k = 0; k < 8; ++k) {
+    e[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[k]);
+    r[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[k]);
+    s[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[k]);
+    acc += e[k] ^ r[k] ^ s[k];
+  }
   t[1] = wall_clock64();
   uint32_t u1[8], u2[8];
-  ecdsa_scalars_plain_inv(e, r, s, u1, u2);
-  acc += u1[0] ^ u2[0];
+  fe rm, rnm;
+  bool rn_ok;
+  wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
+  acc += u1[0] ^ u2[0] ^ rm.v[0];
   t[2] = wall_clock64();
   const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
   xyzz_s P;
@@ -38,11 +47,15 @@ __global__ void __launch_bounds__(64) probe(const uint8_t* hashes, const uint8_t
   wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
   acc += P.x.v[0] ^ (uint32_t)exc;
   t[3] = wall_clock64();
-  const bool ok = ecdsa_check(P, !inf, r);
+  const bool ok = wave_check(P, !inf, rm, rnm, rn_ok);
   acc += ok;
   t[4] = wall_clock64();
+  fe D;
+  inv_mod_n_wave(D, s);
+  acc += D.v[3];
+  t[5] = wall_clock64();
   if (threadIdx.x == 0) {
-    for (int k = 0; k < 4; ++k) stamps[i * 4 + k] = t[k + 1] - t[k];
+    for (int k = 0; k < 5; ++k) stamps[i * 5 + k] = t[k + 1] - t[k];
     sink[i] = acc;
   }
 }
@@ -69,7 +82,7 @@ int main() {
   CHECK(hipMalloc(&dkeys, 64));
   CHECK(hipMalloc(&dvalid, 64));
   CHECK(hipMalloc(&dsink, 4 * n));
-  CHECK(hipMalloc(&dst, 8 * 4 * n));
+  CHECK(hipMalloc(&dst, 8 * 5 * n));
   CHECK(hipMemcpy(dh, h.data(), h.size(), hipMemcpyHostToDevice));
   CHECK(hipMemcpy(ds, sg.data(), sg.size(), hipMemcpyHostToDevice));
   CHECK(hipMemset(dk, 0, 4 * n));
@@ -94,14 +107,14 @@ int main() {
                        reinterpret_cast<const uint4*>(gt), reinterpret_cast<const uint4*>(qt), dst, dsink);
     CHECK(hipDeviceSynchronize());
   }
-  std::vector<uint64_t> st(4 * n);
-  CHECK(hipMemcpy(st.data(), dst, 8 * 4 * n, hipMemcpyDeviceToHost));
-  const char* names[4] = {"inputs", "scalars", "quad_comb", "check"};
-  double sum[4] = {0, 0, 0, 0};
+  std::vector<uint64_t> st(5 * n);
+  CHECK(hipMemcpy(st.data(), dst, 8 * 5 * n, hipMemcpyDeviceToHost));
+  const char* names[5] = {"inputs", "scalars", "quad_comb", "check", "inversion_alone"};
+  double sum[5] = {0, 0, 0, 0, 0};
   for (uint32_t i = 0; i < n; ++i)
-    for (int k = 0; k < 4; ++k) sum[k] += st[4 * i + k];
+    for (int k = 0; k < 5; ++k) sum[k] += st[5 * i + k];
   printf("{\"geometry\": [%d, %d]", WG, WQ);
-  for (int k = 0; k < 4; ++k) printf(", \"%s_us\": %.2f", names[k], sum[k] / n * 1e3 / rate_khz);
+  for (int k = 0; k < 5; ++k) printf(", \"%s_us\": %.2f", names[k], sum[k] / n * 1e3 / rate_khz);
   printf("}\n");
   return 0;
 }
