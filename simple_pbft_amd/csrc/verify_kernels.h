@@ -400,8 +400,10 @@ __device__ __forceinline__ void quad_mul(fe& p, int role, const fe& a0, const fe
 // (gx, gy) + (qx, qy), both affine S-type, into XYZZ (mmadd-2008-s, 3 steps);
 // exc if the x-coordinates meet.  Signed-limb arithmetic (fes.h): differences
 // are D-type, X3 is renormalised (S), Y3 stays D-type (only multiplied later).
-__device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, bool& exc, int role, const fe& gx, const fe& gy,
-                                                const fe& qx, const fe& qy) {
+// The idle lane of step 3 computes rz = rm ZZ3 (r ZZ in Montgomery form, for
+// the fused check of the last level).
+__device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, fe& rz, bool& exc, int role, const fe& gx, const fe& gy,
+                                                const fe& qx, const fe& qy, const fe& rm) {
   fe p, rr, pp, r2, ppp, qq, x3, t, a, b, prod;
   fs_sub(p, qx, gx);
   fs_sub(rr, qy, gy);
@@ -415,9 +417,10 @@ __device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, bool& exc, int role, 
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) x3.v[i] = r2.v[i] - ppp.v[i] - (qq.v[i] << 1);
   fs_norm(x3, x3);                                           // X3 = R^2 - PPP - 2Q
   fs_sub(t, qq, x3);
-  quad_mul(prod, role, rr, t, gy, ppp, rr, t, gy, ppp);      // R (Q - X3), Y1 PPP
+  quad_mul(prod, role, rr, t, gy, ppp, rm, pp, rm, pp);      // R (Q - X3), Y1 PPP, r ZZ3
   quad_bcast<0>(a, prod);
   quad_bcast<1>(b, prod);
+  quad_bcast<2>(rz, prod);
   fs_sub(r.y, a, b);
   r.x = x3;
   r.zz = pp;
@@ -426,8 +429,11 @@ __device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, bool& exc, int role, 
 
 // r = P + Q (both finite XYZZ: X, ZZ, ZZZ S-type, Y S- or D-type), add-2008-s
 // in 4 steps of <= 4 products (the Jacobian quad_jadd needs 5); exc if the
-// x-coordinates meet (P == 0).
-__device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, bool& exc, int role, const xyzz_s& P, const xyzz_s& Q) {
+// x-coordinates meet (P == 0).  The idle lane of step 4 computes rz = rm ZZ
+// of the level's result: of r, or of Q / P when the other side is infinity
+// (pinf / qinf), so r ZZ needs no shuffle of its own.
+__device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, fe& rz, bool& exc, int role, const xyzz_s& P,
+                                              const xyzz_s& Q, const fe& rm, bool pinf, bool qinf) {
   fe prod, u1, u2, s1, s2, p, rr, pp, r2, zz12, zzz12, ppp, qq, x3, t, a, b;
   quad_mul(prod, role, P.x, Q.zz, Q.x, P.zz, P.y, Q.zzz, Q.y, P.zzz);      // U1, U2, S1, S2
   quad_bcast<0>(u1, prod);
@@ -449,24 +455,59 @@ __device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, bool& exc, int role, co
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) x3.v[i] = r2.v[i] - ppp.v[i] - (qq.v[i] << 1);
   fs_norm(x3, x3);                                                          // X3 = R^2 - PPP - 2Q
   fs_sub(t, qq, x3);
-  quad_mul(prod, role, rr, t, s1, ppp, zzz12, ppp, zzz12, ppp);             // R (Q - X3), S1 PPP, ZZZ3
+  fe zsel;
+  fe_sel3(zsel, pinf, Q.zz, qinf, P.zz, r.zz);
+  quad_mul(prod, role, rr, t, s1, ppp, zzz12, ppp, rm, zsel);               // R (Q - X3), S1 PPP, ZZZ3, r ZZ
   quad_bcast<0>(a, prod);
   quad_bcast<1>(b, prod);
   quad_bcast<2>(r.zzz, prod);
+  quad_bcast<3>(rz, prod);
   fs_sub(r.y, a, b);                                                        // Y3 = R (Q - X3) - S1 PPP
   r.x = x3;
 }
 
-// quad q = window q: G entry + Q entry, then a butterfly over the quads.
-// exc reports a doubling / cancellation anywhere (the caller reruns the
-// signature with wave_sum_lanes).
+// The last level fused with Go's x-coordinate check (no Y3, ZZZ3, or product
+// with r afterwards): with rz = r ZZ1 from the previous level,
+//   X3 == r ZZ3  <=>  R^2 - PP (P + 2 U1) == (r ZZ1) ZZ2 PP  <=>  R^2 == PP (P + 2 U1 + rz ZZ2),
+// three steps instead of four plus one.  Only for the test against r (the
+// caller takes the full path when r + n < p also has to be tried).
+__device__ __forceinline__ bool quad_xyzz_add_check(bool& exc, int role, const xyzz_s& P, const xyzz_s& Q,
+                                                    const fe& rz) {
+  fe prod, u1, u2, s1, s2, p, rr, pp, r2, rz12, w, t, d;
+  quad_mul(prod, role, P.x, Q.zz, Q.x, P.zz, P.y, Q.zzz, Q.y, P.zzz);      // U1, U2, S1, S2
+  quad_bcast<0>(u1, prod);
+  quad_bcast<1>(u2, prod);
+  quad_bcast<2>(s1, prod);
+  quad_bcast<3>(s2, prod);
+  fs_sub(p, u2, u1);
+  fs_sub(rr, s2, s1);
+  exc = fs_is_zero(p);
+  quad_mul(prod, role, p, p, rr, rr, rz, Q.zz, rz, Q.zz);                   // PP, R^2, r ZZ1 ZZ2
+  quad_bcast<0>(pp, prod);
+  quad_bcast<1>(r2, prod);
+  quad_bcast<2>(rz12, prod);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) w.v[i] = (u1.v[i] << 1) + rz12.v[i];
+  fs_norm(w, w);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) w.v[i] += p.v[i];                // P + 2 U1 + r ZZ12: |limbs| < 2^30
+  fs_mul(t, pp, w);
+  fs_sub(d, r2, t);
+  return fs_is_zero(d);
+}
+
+__device__ __forceinline__ bool wave_check(const xyzz_s& P, bool finite, const fe& rm, const fe& rnm, bool rn_ok);
+
+// quad q = window q: G entry + Q entry, then a butterfly over the quads; the
+// last level fused with the check against r (quad_xyzz_add_check) unless
+// r + n < p (then the full sum and wave_check).  exc reports a doubling /
+// cancellation anywhere (the caller reruns the signature with wave_sum_lanes).
+// Every lane returns the verdict.
 template <int WG, int WQ>
-__device__ __forceinline__ void wave_sum_quads(xyzz_s& P, bool& inf, bool& exc, const uint32_t u1[8],
-                                               const uint32_t u2[8], const uint4* __restrict__ gtab,
-                                               const uint4* __restrict__ qtab) {
+__device__ __forceinline__ bool wave_verify_quads(bool& exc, const uint32_t u1[8], const uint32_t u2[8],
+                                                  const uint4* __restrict__ gtab, const uint4* __restrict__ qtab,
+                                                  const fe& rm, const fe& rnm, bool rn_ok) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
   constexpr int nW = nG > nQ ? nG : nQ;
-  static_assert(nW <= 16, "one quad per window");
+  static_assert(nW > 8 && nW <= 16, "one quad per window, four butterfly levels");
   const int role = threadIdx.x & 3, q = threadIdx.x >> 2;
   digit_stream<WG> s1;
   digit_stream<WQ> s2;
@@ -490,11 +531,12 @@ __device__ __forceinline__ void wave_sum_quads(xyzz_s& P, bool& inf, bool& exc, 
   entry_to_fe(qx, qy, w16);
   fs_cneg(qy, qy, d2 < 0);
   fs_norm(qy, qy);
-  xyzz_s S;
+  xyzz_s S, P;
+  fe rz, rzS;
   bool e0;
-  quad_mmadd_xyzz(S, e0, role, gx, gy, qx, qy);       // every quad runs it; selected below
+  quad_mmadd_xyzz(S, rzS, e0, role, gx, gy, qx, qy, rm);  // every quad runs it; selected below
   exc = d1 != 0 && d2 != 0 && e0;
-  inf = d1 == 0 && d2 == 0;
+  bool inf = d1 == 0 && d2 == 0;
   const bool both = d1 != 0 && d2 != 0, g_only = d1 != 0;
   fe one;
   fe_set(one, kOneP);
@@ -502,8 +544,9 @@ __device__ __forceinline__ void wave_sum_quads(xyzz_s& P, bool& inf, bool& exc, 
   fe_sel3(P.y, both, S.y, g_only, gy, qy);
   fe_sel3(P.zz, both, S.zz, true, one, one);
   fe_sel3(P.zzz, both, S.zzz, true, one, one);
+  fe_sel3(rz, both, rzS, true, rm, rm);  // a lone table point: ZZ = 1, r ZZ = rm
 #pragma unroll 1
-  for (int m = 1; m < nW; m <<= 1) {
+  for (int m = 1; m < 16; m <<= 1) {
     xyzz_s Q;
     shfl_xor_fe(Q.x, P.x, 4 * m);
     shfl_xor_fe(Q.y, P.y, 4 * m);
@@ -511,7 +554,21 @@ __device__ __forceinline__ void wave_sum_quads(xyzz_s& P, bool& inf, bool& exc, 
     shfl_xor_fe(Q.zzz, P.zzz, 4 * m);
     const bool qinf = __shfl_xor((int)inf, 4 * m, 64) != 0;
     bool e;
-    quad_xyzz_add(S, e, role, P, Q);
+    if (m == 8 && !rn_ok) {  // last level, fused with the check (rn_ok is wave-uniform)
+      bool ok;
+      e = false;
+      if (inf || qinf) {     // a lone partial sum (quad-uniform branch): its own X == r ZZ
+        fe d, rzq;
+        if (inf) fs_mul(rzq, rm, Q.zz);
+        fs_sub(d, inf ? Q.x : P.x, inf ? rzq : rz);
+        ok = !(inf && qinf) && fs_is_zero(d);
+      } else {
+        ok = quad_xyzz_add_check(e, role, P, Q, rz);
+      }
+      exc = exc || (e && !inf && !qinf);
+      return ok;
+    }
+    quad_xyzz_add(S, rz, e, role, P, Q, rm, inf, qinf);
     exc = exc || (e && !inf && !qinf);
     fe_sel3(P.x, inf, Q.x, qinf, P.x, S.x);
     fe_sel3(P.y, inf, Q.y, qinf, P.y, S.y);
@@ -519,6 +576,7 @@ __device__ __forceinline__ void wave_sum_quads(xyzz_s& P, bool& inf, bool& exc, 
     fe_sel3(P.zzz, inf, Q.zzz, qinf, P.zzz, S.zzz);
     inf = inf && qinf;
   }
+  return wave_check(P, !inf, rm, rnm, rn_ok);
 }
 
 // ---- latency-path scalars: the inversion spread over the wave --------------
@@ -545,6 +603,46 @@ __device__ __forceinline__ int32_t lane_from_prev(int32_t x) {  // lane j <- lan
 }
 
 __device__ __forceinline__ int32_t center30(uint32_t x) { return (int32_t)(x << 2) >> 2; }
+
+// divsteps30_var (safegcd.h) shaped for the scalar unit, where every
+// instruction of the one wave costs an issue slot: -f^-1 mod 64 is recomputed
+// only when f changes (a swap), and the loop tests its exit at the bottom.
+__device__ __forceinline__ int32_t divsteps30_scalar(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t nfi = f * (f * f - 2u);  // -f^-1 mod 64 (Newton step from f f = 1 mod 8)
+  int i = 30;
+  int z = __builtin_ctz(g | (0xFFFFFFFFu << i));
+  for (;;) {
+    g >>= z;
+    u <<= z;
+    v <<= z;
+    eta -= z;
+    i -= z;
+    if (i == 0) break;
+    if (eta < 0) {  // delta > 0: (f, g) <- (g, -f)
+      eta = -eta;
+      const uint32_t x = f, y = u, w = v;
+      f = g;
+      g = 0u - x;
+      u = q;
+      q = 0u - y;
+      v = r;
+      r = 0u - w;
+      nfi = f * (f * f - 2u);
+    }
+    const int lim = min(eta + 1, i);  // the 6-bit cap is the & 63 (nfi is exact mod 64)
+    const uint32_t w = (g * nfi) & ((1u << lim) - 1u) & 63u;  // -g / f mod 2^min(lim, 6)
+    g += f * w;
+    q += u * w;
+    r += v * w;
+    z = __builtin_ctz(g | (0xFFFFFFFFu << i));
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return eta;
+}
 
 // limb re-centering: carry (x + 2^29) >> 30 one lane up (not out of the top limb)
 __device__ __forceinline__ int32_t limbs_center(int32_t x, bool top) {
@@ -595,14 +693,15 @@ __device__ __forceinline__ void inv_mod_n_wave(fe& D, const uint32_t x[8]) {
     const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(B, 0);
     const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane(A, 16), e0 = (uint32_t)__builtin_amdgcn_readlane(B, 16);
     trans30 t;
-    eta = divsteps30_var(eta, f0, g0, t);
+    eta = divsteps30_scalar(eta, f0, g0, t);
     const int32_t md = center30(0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * kNInv30);
     const int32_t me = center30(0u - ((uint32_t)t.q * d0 + (uint32_t)t.r * e0) * kNInv30);
     const int64_t P = (int64_t)t.u * A + (int64_t)t.v * B + (int64_t)md * (int32_t)nl;
     const int64_t Q = (int64_t)t.q * A + (int64_t)t.r * B + (int64_t)me * (int32_t)nl;
     A = limbs_center(limbs_shift30(P), top);
     B = limbs_center(limbs_shift30(Q), top);
-    if (__ballot(row == 0 && B != 0) == 0) break;  // g == 0: f = +-1, d = +-R x^-1
+    if (it >= 14 && __ballot(row == 0 && B != 0) == 0) break;  // g == 0: f = +-1, d = +-R x^-1 (tested from batch 15:
+    // every input takes >= 17 batches since f starts at n; a batch with g = 0 leaves f and d unchanged)
   }
   uint32_t fl0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), fl1 = (uint32_t)__builtin_amdgcn_readlane(A, 1);
   const bool pos = fl0 + (fl1 << 30) == 1u;  // f = +-1: its value mod 2^32
@@ -737,11 +836,10 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
     const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
     bool inf;
     bool exc = true;
-    if constexpr (nW <= 16) {
-      xyzz_s P;
-      wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
+    if constexpr (nW > 8 && nW <= 16) {
+      const bool okq = wave_verify_quads<WG, WQ>(exc, u1, u2, gtab, qtab, rm, rnm, rn_ok);
       exc = __any(exc);
-      if (!exc) ok = wave_check(P, !inf, rm, rnm, rn_ok);
+      ok = __builtin_amdgcn_readfirstlane((int)okq) != 0;  // lane 0 = quad 0: the all-reduced verdict
     }
     if (exc) {  // windows outnumber the quads, or a doubling somewhere: exact lane-per-window rerun
       jac P;

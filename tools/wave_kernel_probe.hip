@@ -1,7 +1,7 @@
 // wave_kernel_probe.hip -- stage timestamps of the one-wave-per-signature
 // latency kernel (k_ecdsa_wave's body, verify_kernels.h, replicated with
 // wall_clock64() stamps): input loads, scalars (lane-parallel safegcd + one
-// product step), quad comb, check; plus the inversion alone.  Tables: the
+// product step), quad comb with the fused check; plus the inversion alone.  Tables: the
 // n = 4 geometry (29-bit G, one 24-bit key table with Q = G), built with the
 // product's table kernels.  Measurement tool for DESIGN.md (not the product).
 //   make -C simple_pbft_amd && hipcc --offload-arch=gfx950 -O3 -std=c++17 -c tools/wave_kernel_probe.hip -o p.o \
@@ -42,13 +42,11 @@ __global__ void __launch_bounds__(64) probe(const uint8_t* hashes, const uint8_t
   acc += u1[0] ^ u2[0] ^ rm.v[0];
   t[2] = wall_clock64();
   const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
-  xyzz_s P;
-  bool inf, exc;
-  wave_sum_quads<WG, WQ>(P, inf, exc, u1, u2, gtab, qtab);
-  acc += P.x.v[0] ^ (uint32_t)exc;
+  bool exc;
+  const bool okq = wave_verify_quads<WG, WQ>(exc, u1, u2, gtab, qtab, rm, rnm, rn_ok);
+  acc += (uint32_t)okq ^ (uint32_t)exc;
   t[3] = wall_clock64();
-  const bool ok = wave_check(P, !inf, rm, rnm, rn_ok);
-  acc += ok;
+  acc += __builtin_amdgcn_readfirstlane((int)okq);
   t[4] = wall_clock64();
   fe D;
   inv_mod_n_wave(D, s);
@@ -109,7 +107,7 @@ int main() {
   }
   std::vector<uint64_t> st(5 * n);
   CHECK(hipMemcpy(st.data(), dst, 8 * 5 * n, hipMemcpyDeviceToHost));
-  const char* names[5] = {"inputs", "scalars", "quad_comb", "check", "inversion_alone"};
+  const char* names[5] = {"inputs", "scalars", "quad_comb_and_check", "verdict", "inversion_alone"};
   double sum[5] = {0, 0, 0, 0, 0};
   for (uint32_t i = 0; i < n; ++i)
     for (int k = 0; k < 5; ++k) sum[k] += st[5 * i + k];
