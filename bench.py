@@ -464,7 +464,9 @@ def main():
         n = hi - lo
         pub, H, S, K, ok = synth.config4(n_global, n_keys=args.keys, seed=0x50424654)
         H, S, K, ok = H[lo:hi], S[lo:hi], K[lo:hi], ok[lo:hi]
+    t_reg = time.perf_counter()
     valid = ver.register_keys(pub)
+    t_reg = time.perf_counter() - t_reg  # G table + one table per key, built on the device
     assert valid.all()
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
     db = ver.alloc(0, (n + 7) // 8 + 1)
@@ -536,6 +538,7 @@ def main():
                            "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc else None}
         out["kernels"] = kern
         out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
+        out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "what": "pbftv_register_keys: G table + one table per key built on the device (incl. allocation)"}
         if not args.no_extras and ws == 1:
             out["host_path"] = host_path(ver, H, S, K, ok)
             out["host_path_verifies_per_s"] = out["host_path"]["pageable"]["verifies_per_s"]

@@ -288,19 +288,31 @@ int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const 
 /* ---- ECDSA-P256 signatures (Go crypto/ecdsa.Verify semantics) --------- */
 
 /* Register the replica public keys (k * 64 B, X||Y big-endian); replaces any
- * previous table.  out_valid[j] = 1 if key j is a valid P-256 point (0 <= X,Y
- * < p and on the curve); signatures naming an invalid key always fail.  Builds
- * the per-key fixed-base comb tables on every device (W-bit windows: 1.61 GB
- * per key at W = 22, 436 MB at 20, 34 MiB at 16; see pbftv_table_config). */
+ * previous set.  out_valid[j] = 1 if key j is a valid P-256 point (0 <= X,Y < p
+ * and on the curve); signatures naming an invalid key always fail.  Builds the
+ * fixed-base comb tables on every device (one host thread per GPU): the G table
+ * once per context and width, and one table allocation per key.  Geometry: see
+ * pbftv_table_config. */
 int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid);
 
-/* Comb-table geometry chosen at registration: window bits of the G table
- * (16 / 20 / 24 / 26) and of the key tables (24 / 22 / 20 / 16 / 12 / 8) --
- * the pair with the fewest windows (table additions per verify) whose tables
- * fit the device's free HBM minus a 64 GiB reserve (an MI355X with 100 keys:
- * G 26-bit 21.5 GB + keys 22-bit 161 GB); PBFTV_TABLE_BUDGET_MB caps the key
- * tables, PBFTV_GBITS / PBFTV_QBITS force a width -- and the HBM bytes the
- * tables occupy per device. */
+/* Incremental key changes (membership changes without a rebuild of every
+ * table): pbftv_add_keys appends k keys as indices nkeys .. nkeys + k - 1 at the
+ * registered geometry (PBFTV_ENOMEM if their tables do not fit);
+ * pbftv_set_key replaces key `index` (< nkeys) in place.  Both need a prior
+ * pbftv_register_keys and wait for the device's queued work first. */
+int pbftv_add_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid);
+int pbftv_set_key(pbftv_ctx* ctx, uint32_t index, const uint8_t* pub_xy, uint8_t* out_valid);
+
+/* Comb-table geometry chosen at registration and the HBM its tables take per
+ * device.  Window codes: plain W-bit windows (8, 12, 16, 20, 22, 24, 26: 256/W + 1
+ * windows, 2^(W-1) entries of 64 B each) or the mixed codes 21 (5 x 22-bit +
+ * 7 x 21-bit windows: 1.14 GB per key) and 29 (5 x 29 + 4 x 28: 120 GB).  The
+ * pair (G, keys) is the one with the fewest windows in total (= table
+ * additions per verify) whose tables fit the device's free HBM minus a 16 GiB
+ * reserve for batch scratch: on a 288 GB MI355X, 100 keys -> G 29 + keys 21
+ * (9 + 12 windows, 234 GB), 4 keys -> G 29 + keys 24 (5.9 GB each), 1000 keys
+ * -> keys 16 (34 MiB each).  PBFTV_TABLE_BUDGET_MB caps the key tables,
+ * PBFTV_GBITS / PBFTV_QBITS force a width. */
 int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uint64_t* out_table_bytes);
 
 /* Verify n signatures: hashes (n*32), sig_rs (n*64: r||s big-endian),

@@ -33,11 +33,12 @@ struct TableScratchSizes {
   uint64_t entry_lanes;
 };
 TableScratchSizes table_scratch_sizes(int w, uint32_t nbases);
-// Build nb tables (G first when with_g) of width w into tables (nb * table_bytes(w));
-// keys_le: {x[8], y[8]} LE words per key, key0 = first key of this launch;
-// valid[key] written for every key built.
+// Build nb tables (G first when with_g) of width w; table b is written at
+// tabs[b] (a device array of nb pointers to table_bytes(w) each); keys_le:
+// {x[8], y[8]} LE words per key, key0 = first key of this launch; valid[key]
+// written for every key built.
 hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g,
-                               uint32_t* valid, uint32_t* tables, TableScratch& sc, hipStream_t st);
+                               uint32_t* valid, uint32_t* const* tabs, TableScratch& sc, hipStream_t st);
 // stage 1 -> stage 2 records (verify_kernels.h SigRec: 128 B per signature) and
 // the prefix-product scratch of stage 1's batched inversion
 size_t ecdsa_record_bytes(uint64_t n);
@@ -48,11 +49,13 @@ size_t scalar_prefix_bytes(uint64_t n);
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                                 const uint32_t* key_valid, uint32_t nkeys, void* rec, void* prefix,
                                 const uint32_t* pos, hipStream_t st);
-// stage 2: (wg, wq) one of PBFTV_COMBOS; qtabs = nkeys tables of width wq.
+// stage 2: (wg, wq) one of PBFTV_COMBOS; qtabs = device array of the nkeys
+// key tables' addresses (width wq each, one allocation per key).
 // okb == nullptr: records in arrival order, LSB-first bitmap (ceil(n/8) B)
 // written directly; else one byte per signature at its batch index (okb, n B)
 // and launch_pack_bits builds the bitmap.
-hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
+hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab,
+                             const uint32_t* const* qtabs,
                              uint8_t* bitmap, uint8_t* okb, hipStream_t st);
 // stage 0 (optional): key order pos[i] = position of signature i sorted by key
 // (scratch: key_sort_scratch_bytes, pos first).
@@ -69,7 +72,7 @@ struct CombArgs {
   const void* rec;
   uint64_t n;
   const uint32_t* gtab;
-  const uint32_t* qtabs;
+  const uint32_t* const* qtabs;
   uint8_t* bitmap;
   uint8_t* okb;
 };
@@ -81,13 +84,13 @@ struct WaveArgs {
   const uint32_t* key_valid;
   uint32_t nkeys;
   const uint32_t* gtab;
-  const uint32_t* qtabs;
+  const uint32_t* const* qtabs;
   uint8_t* bitmap;
   uint8_t* okbytes;
 };
 hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
                              uint64_t n, const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
-                             const uint32_t* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st);
+                             const uint32_t* const* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st);
 // batches up to this size take the latency path (env PBFTV_WAVE_MAX overrides; 0 disables)
 uint64_t wave_path_max();
 

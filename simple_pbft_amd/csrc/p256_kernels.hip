@@ -24,29 +24,37 @@ constexpr uint32_t kSortMaxKeys = 1024;
 
 // ---------------------------------------------------------------------------
 // Table construction (p256_algo.h, "generic (W-bit) table construction"):
-// three kernels over all bases of a registration.  Base b of a launch is G
-// when with_g && b == 0, else key key0 + b - with_g.
+// three kernels over all bases of a registration, every phase spread over
+// enough lanes to fill the chip (a registration of G alone is 9 windows).
+// Base b of a launch is G when with_g && b == 0, else key key0 + b - with_g;
+// its table is written at tabs[b] (a device array of per-base pointers: every
+// key table is its own allocation, so keys can be added or replaced one at a
+// time).
 template <int W>
 struct TabGeom {
   using G = CombGeom<W>;
   // L table: (lo+1) B_i, lo < CL; H table: hi (CL B_i), 1 <= hi < NH.  Up to
-  // W = 16 CL = 256; wider windows split E = CL * NH near sqrt(E) so neither
-  // phase-2 walk gets long (W = 20: 1024 x 512, W = 24: 4096 x 2048,
-  // W = 26: 8192 x 4096).
+  // W = 16 CL = 256; wider windows split E = CL * NH near sqrt(E).
   static constexpr int CL = G::kEnt < 256 ? G::kEnt : (G::kW <= 16 ? 256 : 1 << (G::kW / 2));
   static constexpr int NH = G::kEnt / CL;
-  static constexpr int PC = CL < 64 ? CL : 64;              // entries per phase-3 lane
-  static constexpr int SS = 4 * (CL > NH - 1 ? CL : NH - 1);  // phase-2 scratch slots per lane
+  static constexpr int LOG_CL = __builtin_ctz(CL);
+  // phase 2: lanes of SEG consecutive multiples (L: SL segments, H: SH)
+  static constexpr int SEG = CL < 64 ? CL : 64;
+  static constexpr int SL = CL / SEG;
+  static constexpr int SH = NH > 1 ? (NH - 1 + SEG - 1) / SEG : 0;
+  static constexpr int SS = 4 * SEG;  // phase-2 scratch slots per lane
+  // phase 3: lanes of PC entries sharing one H (one batched inversion each)
+  static constexpr int PC = CL < 256 ? CL : 256;
 };
 
-__device__ __forceinline__ bool load_base(const uint32_t* __restrict__ keys_le, uint32_t key0, uint32_t b, int with_g,
-                                          fe& bx, fe& by) {
+__device__ __forceinline__ bool load_base(const uint32_t* __restrict__ keys_le, uint32_t b, int with_g, fe& bx,
+                                          fe& by) {
   if (with_g && b == 0) {
     fe_set(bx, kGxMont);
     fe_set(by, kGyMont);
     return true;
   }
-  const uint32_t* k = keys_le + (uint64_t)(key0 + b - with_g) * 16;
+  const uint32_t* k = keys_le + (uint64_t)(b - with_g) * 16;  // this launch's keys
   uint32_t xw[8], yw[8];
   for (int i = 0; i < 8; ++i) { xw[i] = k[i]; yw[i] = k[8 + i]; }
   if (key_check(xw, yw, bx, by)) return true;
@@ -65,40 +73,94 @@ __global__ void __launch_bounds__(64) k_tab_bases(const uint32_t* __restrict__ k
   if (lane >= nb * nwin) return;
   const uint32_t b = lane / nwin, win = lane % nwin;
   fe bx, by;
-  const bool ok = load_base(keys_le, key0, b, with_g, bx, by);
+  const bool ok = load_base(keys_le, b, with_g, bx, by);
   if (win == 0 && !(with_g && b == 0)) valid[key0 + b - with_g] = ok ? 1u : 0u;
   window_base(bases + (uint64_t)lane * 16, CombGeom<W>::bit((int)win), bx, by);
 }
 
-// phase 2: lane (b, win) -> L = (lo+1) B_i (CL points) and H = hi (CL B_i) (NH-1 points)
+// t P (Jacobian) for 1 <= t < 2^31 and affine P: left-to-right binary method
+// (never exceptional: the running multiple is >= 2 before every addition)
+__device__ __forceinline__ void jac_mul_small(jac& r, uint32_t t, const fe& px, const fe& py) {
+  r.x = px;
+  r.y = py;
+  fe_set(r.z, kOneP);
+  for (int k = 30 - __builtin_clz(t); k >= 0; --k) {
+    jac_double(r, r);
+    if ((t >> k) & 1u) jac_madd<false>(r, px, py);
+  }
+}
+
+// phase 2: lane (bw, seg) with bw = b*nwin + win.  seg < SL: L entries
+// seg*SEG .. +SEG-1, i.e. (k + 1) B_i; seg >= SL: H entries (hi - 1 for hi =
+// 1 + (seg-SL)*SEG ..), i.e. hi (CL B_i).  Each lane starts from its first
+// multiple (binary method) and walks the rest by mixed additions, then one
+// batched inversion to affine.
 template <int W>
 __global__ void __launch_bounds__(64) k_tab_small(const uint32_t* __restrict__ bases, uint32_t nb,
                                                   uint32_t* __restrict__ lbuf, uint32_t* __restrict__ hbuf,
                                                   fe* __restrict__ scratch) {
   using T = TabGeom<W>;
   constexpr int nwin = CombGeom<W>::kWin;
-  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lane >= nb * nwin) return;
-  fe* sc = scratch + (uint64_t)lane * T::SS;
+  constexpr uint32_t segs = T::SL + T::SH;
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= (uint64_t)nb * nwin * segs) return;
+  const uint64_t bw = lane / segs;
+  const uint32_t seg = (uint32_t)(lane % segs);
+  fe* sc = scratch + lane * T::SS;
   auto st = [&](int slot, const fe& v) { sc[slot] = v; };
   auto ld = [&](int slot, fe& v) { v = sc[slot]; };
-  uint32_t bw[16];
-  for (int i = 0; i < 16; ++i) bw[i] = bases[(uint64_t)lane * 16 + i];
-  uint32_t* L = lbuf + (uint64_t)lane * T::CL * 16;
-  multiples(L, T::CL, bw, st, ld);
-  if (T::NH > 1) {
-    uint32_t mw[16];
-    for (int i = 0; i < 16; ++i) mw[i] = L[(uint64_t)(T::CL - 1) * 16 + i];
-    multiples(hbuf + (uint64_t)lane * (T::NH - 1) * 16, T::NH - 1, mw, st, ld);
+  uint32_t bw16[16];
+  for (int i = 0; i < 16; ++i) bw16[i] = bases[bw * 16 + i];
+  fe px, py;
+  entry_to_fe(px, py, bw16);
+  const bool is_h = seg >= (uint32_t)T::SL;
+  uint32_t first, cnt;
+  uint32_t* out;
+  if (!is_h) {
+    first = seg * T::SEG + 1;
+    cnt = T::SEG;
+    out = lbuf + (bw * T::CL + (uint64_t)seg * T::SEG) * 16;
+  } else {  // H walks multiples of Q = CL B_i: 2^LOG_CL doublings, then affine
+    const uint32_t h0 = (seg - T::SL) * T::SEG;
+    first = h0 + 1;
+    cnt = (uint32_t)(T::NH - 1) - h0 < (uint32_t)T::SEG ? (uint32_t)(T::NH - 1) - h0 : (uint32_t)T::SEG;
+    out = hbuf + (bw * (T::NH - 1) + h0) * 16;
+    jac q;
+    q.x = px;
+    q.y = py;
+    fe_set(q.z, kOneP);
+    for (int k = 0; k < T::LOG_CL; ++k) jac_double(q, q);
+    fe zi;
+    fe_inv(zi, q.z);
+    uint32_t qw[16];
+    jac_to_affine_words(qw, q, zi);
+    entry_to_fe(px, py, qw);
   }
+  jac cur;
+  jac_mul_small(cur, first, px, py);
+  for (uint32_t k = 0; k < cnt; ++k) {
+    if (k > 0) {
+      if (first + k - 1 == 1) jac_double(cur, cur);  // 1 P + P
+      else jac_madd<false>(cur, px, py);             // (m + 1) P, 2 <= m << n: never exceptional
+    }
+    st(3 * (int)k, cur.x);
+    st(3 * (int)k + 1, cur.y);
+    st(3 * (int)k + 2, cur.z);
+  }
+  batch_to_affine(out, (int)cnt, st, ld);
 }
 
-// phase 3: lane (b, win, hi, part) -> PC entries idx = hi*CL + part*PC + j of base b's table.
+// phase 3: lane (b, win, hi, part) -> PC entries idx = hi*CL + part*PC + j of
+// base b's table, entry = H_hi + L_lo by AFFINE addition with the PC
+// denominators inverted together: lambda = (ly - hy) / (lx - hx),
+// x3 = lambda^2 - hx - lx, y3 = lambda (hx - x3) - hy -- 6 products per entry
+// plus 1/PC of an inversion.  The one doubling (hi = 1, lo + 1 = CL: L = H)
+// is done in Jacobian form with its own inversion.
 // A launch covers global lanes [lane0, lane1); scratch is indexed by lane - lane0.
 template <int W>
 __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__ lbuf,
                                                     const uint32_t* __restrict__ hbuf, uint64_t lane0,
-                                                    uint64_t lane1, uint32_t* __restrict__ tables,
+                                                    uint64_t lane1, uint32_t* const* __restrict__ tabs,
                                                     fe* __restrict__ scratch) {
   using T = TabGeom<W>;
   using G = CombGeom<W>;
@@ -115,26 +177,79 @@ __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__
   if ((uint64_t)hi * T::CL >= (uint64_t)G::ent((int)win)) return;  // narrow top window: half the entries
   const uint64_t bw = (uint64_t)b * G::kWin + win;  // (base, window) index into lbuf/hbuf
   const uint32_t* L = lbuf + (bw * T::CL + (uint64_t)part * T::PC) * 16;
-  uint32_t hw[16] = {0};
-  if (hi > 0)
-    for (int i = 0; i < 16; ++i) hw[i] = hbuf[(bw * (T::NH - 1) + hi - 1) * 16 + i];
-  uint32_t* out = tables + (uint64_t)b * G::kWords + (G::base((int)win) + (uint64_t)hi * T::CL +
-                                                      (uint64_t)part * T::PC) * 16;
-  fe* sc = scratch + local * 4 * T::PC;
-  sums_chunk(out, T::PC, hi > 0, hw, L, [&](int slot, const fe& v) { sc[slot] = v; },
-             [&](int slot, fe& v) { v = sc[slot]; });
+  uint32_t* out = tabs[b] + (G::base((int)win) + (uint64_t)hi * T::CL + (uint64_t)part * T::PC) * 16;
+  if (hi == 0) {  // H_0 = 0: a copy of L
+    for (int j = 0; j < T::PC * 16; ++j) out[j] = L[j];
+    return;
+  }
+  uint32_t hw[16];
+  for (int i = 0; i < 16; ++i) hw[i] = hbuf[(bw * (T::NH - 1) + hi - 1) * 16 + i];
+  fe hx, hy;
+  entry_to_fe(hx, hy, hw);
+  // the doubling entry of this chunk, if any: lo + 1 = CL with hi = 1
+  const int dbl = (hi == 1 && part == parts - 1) ? T::PC - 1 : -1;
+  fe* pre = scratch + local * T::PC;
+  fe acc, lx, ly, d;
+  fe_set(acc, kOneP);
+  for (int j = 0; j < T::PC; ++j) {
+    entry_to_fe(lx, ly, L + (uint64_t)j * 16);
+    fe_sub(d, lx, hx);
+    if (j == dbl) fe_set(d, kOneP);
+    fe_mul(acc, acc, d);
+    pre[j] = acc;  // d_0 ... d_j
+  }
+  fe inv;
+  fe_inv(inv, acc);
+  for (int j = T::PC - 1; j >= 0; --j) {
+    entry_to_fe(lx, ly, L + (uint64_t)j * 16);
+    fe_sub(d, lx, hx);
+    if (j == dbl) fe_set(d, kOneP);
+    fe dinv;
+    if (j > 0) {
+      fe_mul(dinv, inv, pre[j - 1]);  // 1/d_j
+      fe_mul(inv, inv, d);            // 1/(d_0 ... d_{j-1})
+    } else {
+      dinv = inv;
+    }
+    uint32_t* o = out + (uint64_t)j * 16;
+    if (j == dbl) {  // 2 H
+      jac p;
+      p.x = hx;
+      p.y = hy;
+      fe_set(p.z, kOneP);
+      jac_double(p, p);
+      fe zi;
+      fe_inv(zi, p.z);
+      jac_to_affine_words(o, p, zi);
+      continue;
+    }
+    fe dy, lam, l2, x3, t, y3;
+    fe_sub(dy, ly, hy);
+    fe_mul(lam, dy, dinv);
+    fe_sqr(l2, lam);
+    fe_add(t, hx, lx);
+    fe_sub(x3, l2, t);            // lambda^2 - hx - lx
+    fe_sub(t, hx, x3);
+    fe_mul(y3, lam, t);
+    fe_sub(y3, y3, hy);           // lambda (hx - x3) - hy
+    fe_canon(x3, x3);
+    fe_canon(y3, y3);
+    fe_to_words(o, x3);
+    fe_to_words(o + 8, y3);
+  }
 }
 
 template <int W>
 hipError_t build_tables_w(const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g, uint32_t* valid,
-                          uint32_t* tables, TableScratch& sc, hipStream_t st) {
+                          uint32_t* const* tabs, TableScratch& sc, hipStream_t st) {
   using T = TabGeom<W>;
   using G = CombGeom<W>;
   if (nb == 0) return hipSuccess;
-  const uint32_t lanes12 = nb * G::kWin;
-  hipLaunchKernelGGL(k_tab_bases<W>, dim3((lanes12 + 63) / 64), dim3(64), 0, st, keys_le, key0, nb, with_g, valid,
+  const uint32_t lanes1 = nb * G::kWin;
+  hipLaunchKernelGGL(k_tab_bases<W>, dim3((lanes1 + 63) / 64), dim3(64), 0, st, keys_le, key0, nb, with_g, valid,
                      reinterpret_cast<uint32_t*>(sc.bases));
-  hipLaunchKernelGGL(k_tab_small<W>, dim3((lanes12 + 63) / 64), dim3(64), 0, st,
+  const uint64_t lanes2 = (uint64_t)lanes1 * (T::SL + T::SH);
+  hipLaunchKernelGGL(k_tab_small<W>, dim3((uint32_t)((lanes2 + 63) / 64)), dim3(64), 0, st,
                      reinterpret_cast<const uint32_t*>(sc.bases), nb, reinterpret_cast<uint32_t*>(sc.lbuf),
                      reinterpret_cast<uint32_t*>(sc.hbuf), reinterpret_cast<fe*>(sc.small_scratch));
   // phase 3 in slices of sc.entry_lanes lanes (its scratch is per lane)
@@ -144,7 +259,7 @@ hipError_t build_tables_w(const uint32_t* keys_le, uint32_t key0, uint32_t nb, i
     const uint64_t l1 = total - l0 < sc.entry_lanes ? total : l0 + sc.entry_lanes;
     hipLaunchKernelGGL(k_tab_entries<W>, dim3((uint32_t)((l1 - l0 + 63) / 64)), dim3(64), 0, st,
                        reinterpret_cast<const uint32_t*>(sc.lbuf), reinterpret_cast<const uint32_t*>(sc.hbuf), l0, l1,
-                       tables, reinterpret_cast<fe*>(sc.entry_scratch));
+                       tabs, reinterpret_cast<fe*>(sc.entry_scratch));
   }
   return hipGetLastError();
 }
@@ -157,11 +272,11 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
     z.bases = (size_t)nb * G::kWin * 64;
     z.lbuf = (size_t)nb * G::kWin * T::CL * 64;
     z.hbuf = (size_t)nb * G::kWin * (T::NH > 1 ? T::NH - 1 : 1) * 64;
-    z.small_scratch = (size_t)nb * G::kWin * T::SS * sizeof(fe);
+    z.small_scratch = (size_t)nb * G::kWin * (T::SL + T::SH) * T::SS * sizeof(fe);
     const uint64_t total = (uint64_t)G::kWin * T::NH * (T::CL / T::PC) * nb;
-    const uint64_t cap = 1ull << 17;  // 128 Ki lanes x 9 KiB of scratch
+    const uint64_t cap = 1ull << 18;  // 256 Ki lanes x 9 KiB of scratch
     z.entry_lanes = total < cap ? total : cap;
-    z.entry_scratch = (size_t)z.entry_lanes * 4 * T::PC * sizeof(fe);
+    z.entry_scratch = (size_t)z.entry_lanes * T::PC * sizeof(fe);
   };
   switch (w) {
 #define PBFTV_W(W) \
@@ -194,10 +309,10 @@ int table_windows(int w) {
 }
 
 hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, uint32_t nb, int with_g,
-                               uint32_t* valid, uint32_t* tables, TableScratch& sc, hipStream_t st) {
+                               uint32_t* valid, uint32_t* const* tabs, TableScratch& sc, hipStream_t st) {
   switch (w) {
 #define PBFTV_W(W) \
-  case W: return build_tables_w<W>(keys_le, key0, nb, with_g, valid, tables, sc, st);
+  case W: return build_tables_w<W>(keys_le, key0, nb, with_g, valid, tabs, sc, st);
     PBFTV_TABLE_WIDTHS(PBFTV_W)
 #undef PBFTV_W
     default: return hipErrorInvalidValue;
@@ -423,7 +538,7 @@ bool launch_wave_part_small(int wg, int wq, const WaveArgs& a, hipStream_t st);
 
 hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
                              uint64_t n, const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
-                             const uint32_t* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
+                             const uint32_t* const* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   const WaveArgs a{hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes};
@@ -482,7 +597,8 @@ hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, cons
   return hipGetLastError();
 }
 
-hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs,
+hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab,
+                             const uint32_t* const* qtabs,
                              uint8_t* bitmap, uint8_t* okb, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const CombArgs a{rec, n, gtab, qtabs, bitmap, okb};

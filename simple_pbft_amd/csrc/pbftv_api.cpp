@@ -207,8 +207,10 @@ struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  // signature state: comb table of G (width gbits) and of every registered key (width qbits)
-  DevBuf gtab, qtabs, key_valid;
+  // signature state: comb table of G (width gbits) and one table allocation per
+  // registered key (width qbits), addressed through qptrs (device array, by key)
+  DevBuf gtab, key_valid, qptrs;
+  std::vector<std::unique_ptr<DevBuf>> qtab;
   int gbits = 0, qbits = 0;
   uint32_t nkeys = 0;
   bool have_keys = false;
@@ -531,17 +533,24 @@ int pbftv_open(pbftv_ctx** out, uint32_t device_mask) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(PBFTV_ENODEV, "no HIP devices visible");
   auto ctx = std::make_unique<pbftv_ctx>();
+  // PBFTV_ALIAS_DEVICES=k (tests only): k logical devices per GPU, each with its
+  // own stream, tables and scratch -- the multi-device paths (shards, per-device
+  // registration, bitmap concatenation) on a one-GPU machine.
+  int alias = 1;
+  if (const char* e = getenv("PBFTV_ALIAS_DEVICES")) alias = std::min(8, std::max(1, atoi(e)));
   for (int d = 0; d < count && d < 32; ++d) {
     if (device_mask && !((device_mask >> d) & 1u)) continue;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) continue;  // the kernels are gfx950 code objects
-    auto dev = std::make_unique<Device>();
-    dev->id = d;
-    dev->timing = &ctx->timing;
-    HIP_TRY(hipSetDevice(d));
-    HIP_TRY(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
-    ctx->devs.push_back(std::move(dev));
+    for (int a = 0; a < alias; ++a) {
+      auto dev = std::make_unique<Device>();
+      dev->id = d;
+      dev->timing = &ctx->timing;
+      HIP_TRY(hipSetDevice(d));
+      HIP_TRY(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
+      ctx->devs.push_back(std::move(dev));
+    }
   }
   if (ctx->devs.empty()) return fail(PBFTV_ENODEV, "no gfx950 device in device_mask");
   *out = ctx.release();
@@ -555,7 +564,8 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
-    for (DevBuf* b : {&d->gtab, &d->qtabs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->rec,
+    for (auto& t : d->qtab) t->release();
+    for (DevBuf* b : {&d->gtab, &d->qptrs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->rec,
                       &d->prefix, &d->bitmap, &d->ksort, &d->okb, &d->data, &d->offsets, &d->lengths, &d->order,
                       &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok})
       b->release();  // explicit, with this device current (the destructors are a backstop)
@@ -803,25 +813,28 @@ static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
   *wq = best_q;
 }
 
-static int build_tables(Device& d, int w, const uint32_t* d_keys, uint32_t nb, int with_g, uint32_t* valid,
-                        uint32_t* out) {
+// Build nb tables of width w (G first when with_g) at the addresses tabs[0..nb)
+// (host vector, uploaded here); keys_le: this launch's keys as LE words on the
+// device; valid[key0 + j] written for key j of the launch.
+static int build_tables(Device& d, int w, const uint32_t* d_keys, uint32_t key0, uint32_t nb, int with_g,
+                        uint32_t* valid, const std::vector<void*>& tabs) {
   const pbftv::TableScratchSizes z = pbftv::table_scratch_sizes(w, nb);
-  DevBuf bases, lbuf, hbuf, ssc, esc;
+  DevBuf bases, lbuf, hbuf, ssc, esc, dtabs;
   HIP_TRY(bases.ensure(z.bases));
   HIP_TRY(lbuf.ensure(z.lbuf));
   HIP_TRY(hbuf.ensure(z.hbuf));
   HIP_TRY(ssc.ensure(z.small_scratch));
   HIP_TRY(esc.ensure(z.entry_scratch));
+  HIP_TRY(dtabs.ensure(tabs.size() * sizeof(void*)));
+  HIP_TRY(hipMemcpyAsync(dtabs.p, tabs.data(), tabs.size() * sizeof(void*), hipMemcpyHostToDevice, d.stream));
   pbftv::TableScratch sc{bases.p, lbuf.p, hbuf.p, ssc.p, esc.p, z.entry_lanes};
-  HIP_TRY(pbftv::launch_build_tables(w, d_keys, 0, nb, with_g, valid, out, sc, d.stream));
+  HIP_TRY(pbftv::launch_build_tables(w, d_keys, key0, nb, with_g, valid, dtabs.as<uint32_t* const>(), sc, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
-  for (DevBuf* b : {&bases, &lbuf, &hbuf, &ssc, &esc}) b->release();
   return PBFTV_OK;
 }
 
-int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid) {
-  if (!ctx || (k && !pub_xy)) return fail(PBFTV_EINVAL, "null argument");
-  // big-endian X||Y -> little-endian 32-bit words
+// big-endian X||Y (64 B per key) -> little-endian 32-bit words {x[8], y[8]}
+static std::vector<uint32_t> keys_to_le(const uint8_t* pub_xy, uint32_t k) {
   std::vector<uint32_t> le((size_t)k * 16 + 16);
   for (uint32_t j = 0; j < k; ++j) {
     for (int c = 0; c < 2; ++c) {
@@ -832,44 +845,150 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
       }
     }
   }
+  return le;
+}
+
+// (Re)build the key tables [key0, key0 + k) of d at width d.qbits from host LE
+// words, allocating a table for every index past the current ones; refresh the
+// device pointer array.  valid_out (host, k entries) gets the key check.
+static int build_key_tables(Device& d, const std::vector<uint32_t>& le, uint32_t key0, uint32_t k,
+                            uint32_t* valid_out) {
+  const uint32_t total = std::max<uint32_t>((uint32_t)d.qtab.size(), key0 + k);
+  while (d.qtab.size() < total) {
+    d.qtab.push_back(std::make_unique<DevBuf>());
+    HIP_TRY(d.qtab.back()->ensure(pbftv::table_bytes(d.qbits)));
+  }
+  // key_valid grows with the key count (old flags kept)
+  if (d.key_valid.cap < (size_t)total * 4) {
+    DevBuf nv;
+    HIP_TRY(nv.ensure((size_t)total * 4));
+    if (key0 > 0) HIP_TRY(hipMemcpyAsync(nv.p, d.key_valid.p, (size_t)key0 * 4, hipMemcpyDeviceToDevice, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    std::swap(d.key_valid.p, nv.p);
+    std::swap(d.key_valid.cap, nv.cap);
+  }
+  std::vector<void*> tabs(k);
+  for (uint32_t j = 0; j < k; ++j) tabs[j] = d.qtab[key0 + j]->p;
+  DevBuf keys;
+  HIP_TRY(keys.ensure((size_t)k * 64 + 64));
+  HIP_TRY(hipMemcpyAsync(keys.p, le.data(), (size_t)k * 64, hipMemcpyHostToDevice, d.stream));
+  if (k) {
+    int rc = build_tables(d, d.qbits, keys.as<uint32_t>(), key0, k, 0, d.key_valid.as<uint32_t>(), tabs);
+    if (rc != PBFTV_OK) return rc;
+  }
+  std::vector<void*> ptrs(total);
+  for (uint32_t j = 0; j < total; ++j) ptrs[j] = d.qtab[j]->p;
+  HIP_TRY(d.qptrs.ensure((size_t)std::max<uint32_t>(total, 1) * sizeof(void*)));
+  if (total)
+    HIP_TRY(hipMemcpyAsync(d.qptrs.p, ptrs.data(), total * sizeof(void*), hipMemcpyHostToDevice, d.stream));
+  if (valid_out && k)
+    HIP_TRY(hipMemcpyAsync(valid_out, d.key_valid.as<uint32_t>() + key0, (size_t)k * 4, hipMemcpyDeviceToHost,
+                           d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  d.nkeys = total;
+  return PBFTV_OK;
+}
+
+extern "C++" {
+// fn(device) on every device of the context: one host thread per device when
+// they are distinct GPUs (the table builds of a registration run in
+// parallel), in turn when logical devices share a GPU (PBFTV_ALIAS_DEVICES).
+template <class Fn>
+static int for_each_device(pbftv_ctx* ctx, Fn fn) {
+  bool shared = false;
+  for (size_t a = 0; a < ctx->devs.size(); ++a)
+    for (size_t b = a + 1; b < ctx->devs.size(); ++b) shared |= ctx->devs[a]->id == ctx->devs[b]->id;
+  if (ctx->devs.size() == 1 || shared) {
+    for (auto& dp : ctx->devs) {
+      int rc = fn(*dp, dp.get() == ctx->devs[0].get());
+      if (rc != PBFTV_OK) return rc;
+    }
+    return PBFTV_OK;
+  }
+  std::vector<int> rc(ctx->devs.size(), PBFTV_OK);
+  std::vector<std::string> errs(ctx->devs.size());
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < ctx->devs.size(); ++i)
+    th.emplace_back([&, i] {
+      rc[i] = fn(*ctx->devs[i], i == 0);
+      if (rc[i] != PBFTV_OK) errs[i] = g_last_error;
+    });
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < rc.size(); ++i)
+    if (rc[i] != PBFTV_OK) return fail(rc[i], errs[i]);
+  return PBFTV_OK;
+}
+}  // extern "C++"
+
+int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid) {
+  if (!ctx || (k && !pub_xy)) return fail(PBFTV_EINVAL, "null argument");
+  const std::vector<uint32_t> le = keys_to_le(pub_xy, k);
   std::vector<uint32_t> valid(k ? k : 1, 0);
-  bool first = true;
-  for (auto& dp : ctx->devs) {
-    Device& d = *dp;
+  int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
     d.have_keys = false;
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    for (auto& t : d.qtab) t->release();  // the old key tables go first: their HBM counts for the new ones
+    d.qtab.clear();
+    d.nkeys = 0;
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     int wg, wq;
-    choose_bits(k, free_b + d.qtabs.cap + d.gtab.cap, &wg, &wq);
+    choose_bits(k, free_b + d.gtab.cap, &wg, &wq);
     if (d.gbits != wg) {  // G table: once per context (and width)
+      d.gtab.release();
       HIP_TRY(d.gtab.ensure(pbftv::table_bytes(wg)));
       DevBuf dummy;
       HIP_TRY(dummy.ensure(64));
-      int rc = build_tables(d, wg, nullptr, 1, 1, dummy.as<uint32_t>(), d.gtab.as<uint32_t>());
-      dummy.release();
-      if (rc != PBFTV_OK) return rc;
+      const int r = build_tables(d, wg, nullptr, 0, 1, 1, dummy.as<uint32_t>(), {d.gtab.p});
+      if (r != PBFTV_OK) return r;
       d.gbits = wg;
     }
-    HIP_TRY(d.qtabs.ensure((size_t)(k ? k : 1) * pbftv::table_bytes(wq)));
-    HIP_TRY(d.key_valid.ensure((size_t)(k ? k : 1) * 4));
-    DevBuf keys;
-    HIP_TRY(keys.ensure(le.size() * 4));
-    HIP_TRY(hipMemcpyAsync(keys.p, le.data(), le.size() * 4, hipMemcpyHostToDevice, d.stream));
-    if (k) {
-      int rc = build_tables(d, wq, keys.as<uint32_t>(), k, 0, d.key_valid.as<uint32_t>(), d.qtabs.as<uint32_t>());
-      if (rc != PBFTV_OK) return rc;
-    }
-    if (first && k) HIP_TRY(hipMemcpy(valid.data(), d.key_valid.p, (size_t)k * 4, hipMemcpyDeviceToHost));
-    keys.release();
     d.qbits = wq;
-    d.nkeys = k;
+    const int r = build_key_tables(d, le, 0, k, first ? valid.data() : nullptr);
+    if (r != PBFTV_OK) return r;
     d.have_keys = true;
-    first = false;
-  }
+    return PBFTV_OK;
+  });
+  if (rc != PBFTV_OK) return rc;
   if (out_valid)
     for (uint32_t j = 0; j < k; ++j) out_valid[j] = valid[j] ? 1 : 0;
+  return PBFTV_OK;
+}
+
+int pbftv_add_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid) {
+  if (!ctx || (k && !pub_xy)) return fail(PBFTV_EINVAL, "null argument");
+  if (!keys_ready(ctx)) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  const std::vector<uint32_t> le = keys_to_le(pub_xy, k);
+  std::vector<uint32_t> valid(k ? k : 1, 0);
+  int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return build_key_tables(d, le, d.nkeys, k, first ? valid.data() : nullptr);
+  });
+  if (rc != PBFTV_OK) return rc;
+  if (out_valid)
+    for (uint32_t j = 0; j < k; ++j) out_valid[j] = valid[j] ? 1 : 0;
+  return PBFTV_OK;
+}
+
+int pbftv_set_key(pbftv_ctx* ctx, uint32_t index, const uint8_t* pub_xy, uint8_t* out_valid) {
+  if (!ctx || !pub_xy) return fail(PBFTV_EINVAL, "null argument");
+  if (!keys_ready(ctx)) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
+  for (auto& dp : ctx->devs)
+    if (index >= dp->nkeys) return fail(PBFTV_EINVAL, "key index out of range");
+  const std::vector<uint32_t> le = keys_to_le(pub_xy, 1);
+  uint32_t valid = 0;
+  int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(hipStreamSynchronize(d.stream));  // no verify still reads the old table
+    return build_key_tables(d, le, index, 1, first ? &valid : nullptr);
+  });
+  if (rc != PBFTV_OK) return rc;
+  if (out_valid) *out_valid = valid ? 1 : 0;
   return PBFTV_OK;
 }
 
@@ -890,7 +1009,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   if (n <= pbftv::wave_path_max()) {
     HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, st, [&] {
       return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(),
-                                      d.nkeys, d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(), d_bitmap, nullptr, st);
+                                      d.nkeys, d.gtab.as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), d_bitmap, nullptr, st);
     }));
     return PBFTV_OK;
   }
@@ -909,7 +1028,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
                                        d.prefix.p, pos, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
-    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.rec.p, n, d.gtab.as<uint32_t>(), d.qtabs.as<uint32_t>(),
+    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.rec.p, n, d.gtab.as<uint32_t>(), d.qptrs.as<const uint32_t* const>(),
                                     d_bitmap, sorted ? d.okb.as<uint8_t>() : nullptr, st);
   }));
   if (sorted) HIP_TRY(pbftv::launch_pack_bits(d.okb.as<uint8_t>(), n, d_bitmap, st));
@@ -1010,7 +1129,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
       return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, st8 + oh, st8 + os, reinterpret_cast<uint32_t*>(st8 + ok), n,
                                       d.key_valid.as<uint32_t>(), d.nkeys, d.gtab.as<uint32_t>(),
-                                      d.qtabs.as<uint32_t>(), nullptr, st8 + oo, d.stream);
+                                      d.qptrs.as<const uint32_t* const>(), nullptr, st8 + oo, d.stream);
     }));
     // every wave writes its byte after its last read of the inputs, so once
     // all n bytes are in, the staging area is free for the next call

@@ -191,7 +191,7 @@ __device__ __forceinline__ void read_entry_lds(uint4 (*sent)[256], uint32_t t, u
 template <int WG, int WQ>
 __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigRec* __restrict__ rec, uint64_t n,
                                                                     const uint4* __restrict__ gtab,
-                                                                    const uint4* __restrict__ qtabs,
+                                                                    const uint4* const* __restrict__ qtabs,
                                                                     uint8_t* __restrict__ bitmap,
                                                                     uint8_t* __restrict__ okb) {
   using S = CombSteps<WG, WQ>;
@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigR
       PBFTV_UNROLL for (int j = 0; j < S::nD; ++j)
         sdig[j][t] = (typename S::Digit)((S::is_q(j) ? s2.next() : s1.next()) - 1);
     }
-    const uint4* qtab = qtabs + (uint64_t)meta.x * (CombGeom<WQ>::kWords / 4);
+    const uint4* qtab = qtabs[meta.x];  // the key's own table allocation
     xyzz_s R;  // signed-limb accumulator (fes.h)
     bool inf = true;
     int d = (int)sdig[0][t] + 1;
@@ -813,7 +813,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
                                                    const uint8_t* __restrict__ sigs,
                                                    const uint32_t* __restrict__ key_idx, uint64_t n,
                                                    const uint32_t* __restrict__ key_valid, uint32_t nkeys,
-                                                   const uint4* __restrict__ gtab, const uint4* __restrict__ qtabs,
+                                                   const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
                                                    uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
   constexpr int nW = nG > nQ ? nG : nQ;
@@ -833,7 +833,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
     fe rm, rnm;
     bool rn_ok;
     wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
-    const uint4* qtab = qtabs + (uint64_t)key_idx[i] * (CombGeom<WQ>::kWords / 4);
+    const uint4* qtab = qtabs[key_idx[i]];
     bool inf;
     bool exc = true;
     if constexpr (nW > 8 && nW <= 16) {
@@ -864,20 +864,21 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
 
 template <int WG, int WQ>
 void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
-                          const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab, const uint32_t* qtabs,
+                          const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
+                          const uint32_t* const* qtabs,
                           uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
   hipLaunchKernelGGL((k_ecdsa_wave<WG, WQ>), dim3((uint32_t)n), dim3(64), 0, st, hashes, sigs, key_idx, n, key_valid,
-                     nkeys, reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4*>(qtabs), bitmap,
+                     nkeys, reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4* const*>(qtabs), bitmap,
                      okbytes);
 }
 
 template <int WG, int WQ>
-void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* qtabs, uint8_t* bitmap,
+void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* const* qtabs, uint8_t* bitmap,
                    uint8_t* okb, hipStream_t st) {
   const uint64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL((k_ecdsa_comb<WG, WQ>), dim3((uint32_t)blocks), dim3(256), 0, st,
                      reinterpret_cast<const SigRec*>(rec), n, reinterpret_cast<const uint4*>(gtab),
-                     reinterpret_cast<const uint4*>(qtabs), bitmap, okb);
+                     reinterpret_cast<const uint4* const*>(qtabs), bitmap, okb);
 }
 
 // One instantiation unit: the dispatchers for the geometry pairs COMBOS(X).

@@ -123,6 +123,8 @@ def lib() -> ctypes.CDLL:
         "pbftv_verify_msg_batch": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _vp, ctypes.c_uint64, _vp, _vp,
                                                   _vp, _vp, _vp, _vp]),
         "pbftv_register_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+        "pbftv_add_keys": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+        "pbftv_set_key": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp]),
         "pbftv_table_config": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                               ctypes.POINTER(ctypes.c_uint64)]),
         "pbftv_ecdsa_p256_verify_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
@@ -704,6 +706,21 @@ class Verifier:
         valid = np.zeros(max(k, 1), np.uint8)
         _check(self._L.pbftv_register_keys(self._h, pub_xy.ctypes.data, k, valid.ctypes.data))
         return valid[:k].astype(bool)
+
+    def add_keys(self, pub_xy: np.ndarray) -> np.ndarray:
+        """pbftv_add_keys: append keys (indices after the registered ones); their validity."""
+        pub_xy = np.ascontiguousarray(pub_xy, np.uint8).reshape(-1, 64)
+        k = pub_xy.shape[0]
+        valid = np.zeros(max(k, 1), np.uint8)
+        _check(self._L.pbftv_add_keys(self._h, pub_xy.ctypes.data, k, valid.ctypes.data))
+        return valid[:k].astype(bool)
+
+    def set_key(self, index: int, pub_xy) -> bool:
+        """pbftv_set_key: replace key `index` in place; its validity."""
+        pub = np.ascontiguousarray(pub_xy, np.uint8).reshape(64)
+        valid = np.zeros(1, np.uint8)
+        _check(self._L.pbftv_set_key(self._h, index, pub.ctypes.data, valid.ctypes.data))
+        return bool(valid[0])
 
     def table_config(self):
         """(G window bits, key window bits, table bytes per device)."""

@@ -1,0 +1,129 @@
+"""Key-table management and the in-context multi-device path on hardware.
+
+* pbftv_add_keys / pbftv_set_key: keys appended or replaced one at a time at
+  the registered geometry, each checked against the oracle's verify.
+* PBFTV_ALIAS_DEVICES=2 maps two logical context devices onto GPU 0, so the
+  paths a multi-GPU context takes -- per-device registration, contiguous
+  shards of 512-aligned items, per-shard pipelines / flushes, and the bitmap
+  concatenation at s.lo / 8 -- run here against the oracle, with batch sizes
+  that are not multiples of 512."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import fixture_arrays, oracle_sign_pool
+from oracle import gojson
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_bits(oracle_lib, H, S, K, keys):
+    n = len(K)
+    want = np.zeros((n + 7) // 8 + 1, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(H.ctypes.data, S.ctypes.data, K.ctypes.data, n, keys.ctypes.data,
+                                              len(keys), want.ctypes.data, 8)
+    return np.unpackbits(want, bitorder="little")[:n].astype(bool)
+
+
+@pytest.fixture(params=["wave", "lane"])
+def path(request, monkeypatch):
+    monkeypatch.setenv("PBFTV_WAVE_MAX", "100000000" if request.param == "wave" else "0")
+    return request.param
+
+
+def test_add_and_set_keys(oracle_lib, path, monkeypatch):
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_GBITS", "24")  # small tables: this test is about key bookkeeping
+    monkeypatch.setenv("PBFTV_QBITS", "16")
+    keys, H, S, K = oracle_sign_pool(oracle_lib, 6, 40, seed=71)
+    with Verifier() as v:
+        assert v.register_keys(keys[:3]).all()
+        assert v.table_config()[:2] == (24, 16)
+        # signatures under keys 3..5 fail while those keys are unknown (index out of range)
+        got = v.verify_batch(H, S, K)
+        assert got.tolist() == (K < 3).tolist()
+        assert v.add_keys(keys[3:5]).all()
+        got = v.verify_batch(H, S, K)
+        assert got.tolist() == (K < 5).tolist()
+        assert v.add_keys(keys[5:]).all()
+        assert v.verify_batch(H, S, K).all()
+        assert v.table_config()[2] > 0
+        # replace key 1 by key 4: key 1's signatures now fail, key 4's verify under index 1
+        assert v.set_key(1, keys[4])
+        K2 = K.copy()
+        K2[K == 4] = 1
+        want = _oracle_bits(oracle_lib, H, S, K2, np.concatenate([keys[:1], keys[4:5], keys[2:]]))
+        assert v.verify_batch(H, S, K2).tolist() == want.tolist()
+        assert not v.verify_batch(H[K == 1], S[K == 1], K[K == 1]).any()
+        # an invalid key is reported and its signatures fail
+        bad = keys[0].copy()
+        bad[63] ^= 1
+        assert not v.set_key(2, bad)
+        assert not v.verify_batch(H[K == 2], S[K == 2], K[K == 2]).any()
+        with pytest.raises(Exception):
+            v.set_key(99, keys[0])
+
+
+@pytest.fixture
+def two_devices(monkeypatch):
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_ALIAS_DEVICES", "2")
+    monkeypatch.setenv("PBFTV_GBITS", "24")
+    monkeypatch.setenv("PBFTV_QBITS", "16")
+    v = Verifier()
+    assert v.device_count() == 2 and v.device_id(0) == v.device_id(1)
+    yield v
+    v.close()
+
+
+@pytest.mark.parametrize("n", [2049, 5000, 70001])
+def test_two_device_shards_vs_oracle(two_devices, oracle_lib, n):
+    """Host-buffer verify split over two logical devices (pipelined shards,
+    key order in both at 70001), bitmap joined at the 512-aligned boundary."""
+    v = two_devices
+    keys, h, s, k = oracle_sign_pool(oracle_lib, 10, 30, seed=n)
+    assert v.register_keys(keys).all()
+    rng = np.random.default_rng(n)
+    idx = rng.integers(0, len(k), n)
+    H, S, K = h[idx].copy(), s[idx].copy(), k[idx].copy()
+    bad = rng.choice(n, n // 50, replace=False)
+    S[bad, 5] ^= 0x10
+    got = v.verify_batch(H, S, K)
+    want = np.ones(n, bool)
+    want[bad] = False
+    assert got.tolist() == want.tolist()
+    sample = rng.choice(n, 300, replace=False)
+    assert got[sample].tolist() == _oracle_bits(oracle_lib, H[sample], S[sample], K[sample], keys).tolist()
+
+
+def test_two_device_fixtures_and_flush(two_devices, oracle_lib, ecdsa_fixtures):
+    """Golden vectors tiled past one shard, and a vote flush + SHA batch split
+    over the two devices."""
+    from simple_pbft_amd.pbftv import VoteColumns
+    v = two_devices
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    v.register_keys(keys)
+    reps = 3000 // len(kidx) + 1
+    H, S, K = np.tile(hashes, (reps, 1)), np.tile(sigs, (reps, 1)), np.tile(kidx, reps)
+    assert v.verify_batch(H, S, K).tolist() == np.tile(expect, reps).tolist()
+    n = 3333
+    votes = [(7, i, b"%064x" % (i * 977), b"node%d" % (i % 4), i % 2) for i in range(n)]
+    dg, _, _ = v.flush_votes(VoteColumns(votes))
+    assert [x.tobytes() for x in dg] == [hashlib.sha256(gojson.vote(*x)).digest() for x in votes]
+    msgs = [bytes([i % 251]) * (i % 300) for i in range(n)]
+    data, off, ln = v.pack(msgs)
+    assert [x.tobytes() for x in v.sha256_batch(data, off, ln)] == [hashlib.sha256(m).digest() for m in msgs]
+
+
+def test_two_device_registration_geometry(two_devices, oracle_lib):
+    v = two_devices
+    keys, H, S, K = oracle_sign_pool(oracle_lib, 3, 4, seed=5)
+    assert v.register_keys(keys).all()
+    g, q, b = v.table_config()
+    assert (g, q) == (24, 16) and b > 0
+    assert v.add_keys(keys[:1]).all()          # both logical devices get the new table
+    K2 = np.concatenate([K, np.full(4, 3, np.uint32)])
+    assert v.verify_batch(np.concatenate([H, H[:4]]), np.concatenate([S, S[:4]]), K2).all()

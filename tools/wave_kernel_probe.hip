@@ -94,7 +94,11 @@ int main() {
     CHECK(hipMalloc(&b, z.bases)); CHECK(hipMalloc(&l, z.lbuf)); CHECK(hipMalloc(&hb, z.hbuf));
     CHECK(hipMalloc(&ss, z.small_scratch)); CHECK(hipMalloc(&es, z.entry_scratch));
     TableScratch sc{b, l, hb, ss, es, z.entry_lanes};
-    CHECK(launch_build_tables(w, dkeys, 0, 1, w == WG ? 1 : 0, dvalid, w == WG ? gt : qt, sc, 0));
+    uint32_t** dtab;
+    uint32_t* tab = w == WG ? gt : qt;
+    CHECK(hipMalloc(&dtab, sizeof(void*)));
+    CHECK(hipMemcpy(dtab, &tab, sizeof(void*), hipMemcpyHostToDevice));
+    CHECK(launch_build_tables(w, dkeys, 0, 1, w == WG ? 1 : 0, dvalid, dtab, sc, 0));
     CHECK(hipDeviceSynchronize());
     CHECK(hipFree(b)); CHECK(hipFree(l)); CHECK(hipFree(hb)); CHECK(hipFree(ss)); CHECK(hipFree(es));
   }
