@@ -157,6 +157,7 @@ __global__ void __launch_bounds__(64) k_tab_small(const uint32_t* __restrict__ b
 // plus 1/PC of an inversion.  The one doubling (hi = 1, lo + 1 = CL: L = H)
 // is done in Jacobian form with its own inversion.
 // A launch covers global lanes [lane0, lane1); scratch is indexed by lane - lane0.
+// (2 waves per SIMD at 189 VGPRs: 3 measured the same, 4 spills and is 15 % slower; tools/reg_ab.sh)
 template <int W>
 __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__ lbuf,
                                                     const uint32_t* __restrict__ hbuf, uint64_t lane0,
@@ -188,26 +189,41 @@ __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__
   entry_to_fe(hx, hy, hw);
   // the doubling entry of this chunk, if any: lo + 1 = CL with hi = 1
   const int dbl = (hi == 1 && part == parts - 1) ? T::PC - 1 : -1;
-  fe* pre = scratch + local * T::PC;
+  // signed-limb arithmetic (fes.h): differences are 9 subtractions, products
+  // S-type.  Only the prefix products go to scratch, limb-major across the
+  // launch's lanes (coalesced); d_j is recomputed from L (cache-resident: one
+  // L row serves every hi of its window) on the way back.
+  const uint64_t nl = lane1 - lane0;
+  uint32_t* pre = reinterpret_cast<uint32_t*>(scratch) + local;
+  auto st_pre = [&](int j, const fe& v) {
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) pre[((uint64_t)j * 9 + l) * nl] = v.v[l];
+  };
+  auto ld_pre = [&](int j, fe& v) {
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) v.v[l] = pre[((uint64_t)j * 9 + l) * nl];
+  };
+  auto den = [&](int j, fe& lx, fe& ly, fe& d) {
+    entry_to_fe(lx, ly, L + (uint64_t)j * 16);
+    fs_sub(d, lx, hx);
+    if (j == dbl) fe_set(d, kOneP);
+  };
   fe acc, lx, ly, d;
   fe_set(acc, kOneP);
   for (int j = 0; j < T::PC; ++j) {
-    entry_to_fe(lx, ly, L + (uint64_t)j * 16);
-    fe_sub(d, lx, hx);
-    if (j == dbl) fe_set(d, kOneP);
-    fe_mul(acc, acc, d);
-    pre[j] = acc;  // d_0 ... d_j
+    den(j, lx, ly, d);
+    fs_mul(acc, acc, d);
+    st_pre(j, acc);  // d_0 ... d_j
   }
   fe inv;
+  fs_canon(acc, acc);
   fe_inv(inv, acc);
   for (int j = T::PC - 1; j >= 0; --j) {
-    entry_to_fe(lx, ly, L + (uint64_t)j * 16);
-    fe_sub(d, lx, hx);
-    if (j == dbl) fe_set(d, kOneP);
+    den(j, lx, ly, d);
     fe dinv;
     if (j > 0) {
-      fe_mul(dinv, inv, pre[j - 1]);  // 1/d_j
-      fe_mul(inv, inv, d);            // 1/(d_0 ... d_{j-1})
+      fe p;
+      ld_pre(j - 1, p);
+      fs_mul(dinv, inv, p);  // 1/d_j
+      fs_mul(inv, inv, d);   // 1/(d_0 ... d_{j-1})
     } else {
       dinv = inv;
     }
@@ -224,16 +240,16 @@ __global__ void __launch_bounds__(64) k_tab_entries(const uint32_t* __restrict__
       continue;
     }
     fe dy, lam, l2, x3, t, y3;
-    fe_sub(dy, ly, hy);
-    fe_mul(lam, dy, dinv);
-    fe_sqr(l2, lam);
-    fe_add(t, hx, lx);
-    fe_sub(x3, l2, t);            // lambda^2 - hx - lx
-    fe_sub(t, hx, x3);
-    fe_mul(y3, lam, t);
-    fe_sub(y3, y3, hy);           // lambda (hx - x3) - hy
-    fe_canon(x3, x3);
-    fe_canon(y3, y3);
+    fs_sub(dy, ly, hy);
+    fs_mul(lam, dy, dinv);        // S
+    fs_sqr(l2, lam);
+    PBFTV_UNROLL for (int i = 0; i < 9; ++i) x3.v[i] = l2.v[i] - hx.v[i] - lx.v[i];
+    fs_norm(x3, x3);              // lambda^2 - hx - lx (S)
+    fs_sub(t, hx, x3);            // D
+    fs_mul(y3, lam, t);
+    fs_sub(y3, y3, hy);           // lambda (hx - x3) - hy (D)
+    fs_canon(x3, x3);
+    fs_canon(y3, y3);
     fe_to_words(o, x3);
     fe_to_words(o + 8, y3);
   }
@@ -274,7 +290,7 @@ TableScratchSizes table_scratch_sizes(int w, uint32_t nb) {
     z.hbuf = (size_t)nb * G::kWin * (T::NH > 1 ? T::NH - 1 : 1) * 64;
     z.small_scratch = (size_t)nb * G::kWin * (T::SL + T::SH) * T::SS * sizeof(fe);
     const uint64_t total = (uint64_t)G::kWin * T::NH * (T::CL / T::PC) * nb;
-    const uint64_t cap = 1ull << 18;  // 256 Ki lanes x 9 KiB of scratch
+    const uint64_t cap = 1ull << 18;  // 256 Ki lanes x 9 KiB of prefix products
     z.entry_lanes = total < cap ? total : cap;
     z.entry_scratch = (size_t)z.entry_lanes * T::PC * sizeof(fe);
   };

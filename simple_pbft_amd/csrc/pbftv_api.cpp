@@ -18,6 +18,7 @@
 #include <cstring>
 #include <functional>
 #include <initializer_list>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -207,10 +208,15 @@ struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  // signature state: comb table of G (width gbits) and one table allocation per
-  // registered key (width qbits), addressed through qptrs (device array, by key)
-  DevBuf gtab, key_valid, qptrs;
-  std::vector<std::unique_ptr<DevBuf>> qtab;
+  // signature state: comb table of G (width gbits) and one table per registered
+  // key (width qbits), addressed through qptrs (device array, by key).  Key
+  // tables live in blocks (one per registration / add_keys call; slots beyond
+  // nkeys are spare capacity kept for the next registration at this width).
+  std::shared_ptr<DevBuf> gtab;  // shared by every context on this GPU at this width (g_tables)
+  DevBuf key_valid, qptrs;
+  DevBuf tab_scratch[6];  // table build: bases, L, H, phase-2 / phase-3 scratch, table addresses
+  std::vector<std::unique_ptr<DevBuf>> qblocks;
+  std::vector<void*> qtab;  // table of key j (registered keys first, then spare slots)
   int gbits = 0, qbits = 0;
   uint32_t nkeys = 0;
   bool have_keys = false;
@@ -294,6 +300,11 @@ hipError_t collect_times(Device& d) {
 }
 
 }  // namespace
+
+// G comb tables by (HIP device, width): built once and shared by every
+// context (and aliased logical device) on that GPU while one holds it.
+std::mutex g_tables_mu;
+std::map<std::pair<int, int>, std::weak_ptr<DevBuf>> g_tables;
 
 struct pbftv_ctx {
   std::vector<std::unique_ptr<Device>> devs;
@@ -564,8 +575,10 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
-    for (auto& t : d->qtab) t->release();
-    for (DevBuf* b : {&d->gtab, &d->qptrs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->rec,
+    for (auto& b : d->qblocks) b->release();
+    for (auto& b : d->tab_scratch) b.release();
+    d->gtab.reset();
+    for (DevBuf* b : {&d->qptrs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->rec,
                       &d->prefix, &d->bitmap, &d->ksort, &d->okb, &d->data, &d->offsets, &d->lengths, &d->order,
                       &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok})
       b->release();  // explicit, with this device current (the destructors are a backstop)
@@ -774,14 +787,14 @@ constexpr size_t kTableReserve = 16ull << 30;
 // 9 + 17.  Among equal totals the narrower G wins, and for each G the key
 // width with the fewest windows, then the least HBM (21 before 22: both 12
 // windows).  PBFTV_TABLE_BUDGET_MB caps the key tables.
-static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
+static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq, const std::function<bool(int)>& g_shared) {
   const uint64_t kk = k ? k : 1;
   const char* env_budget = getenv("PBFTV_TABLE_BUDGET_MB");
   const int force_g = env_bits("PBFTV_GBITS", 0), force_q = env_bits("PBFTV_QBITS", 0);
   int best_g = 0, best_q = 0, best_win = 1 << 30;
   for (int g : {16, 20, 24, 26, 29}) {
     if (force_g && g != force_g) continue;
-    const size_t gb = pbftv::table_bytes(g);
+    const size_t gb = g_shared(g) ? 0 : pbftv::table_bytes(g);  // a G table another context built is free
     size_t budget = free_bytes > kTableReserve + gb ? free_bytes - kTableReserve - gb : 0;
     if (g > 16 && budget == 0 && !force_g) continue;  // wide G tables only with room to spare
     if (g <= 26) budget = std::max(budget, free_bytes / 8);
@@ -813,23 +826,37 @@ static void choose_bits(uint32_t k, size_t free_bytes, int* wg, int* wq) {
   *wq = best_q;
 }
 
+// PBFTV_TRACE=1: phase timings of key registration on stderr (diagnostics)
+static void trace(const char* what, int dev, std::chrono::steady_clock::time_point& t0) {
+  static const bool on = getenv("PBFTV_TRACE") != nullptr;
+  const auto t1 = std::chrono::steady_clock::now();
+  if (on) fprintf(stderr, "pbftv[dev %d] %s: %.1f ms\n", dev, what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+  t0 = t1;
+}
+
 // Build nb tables of width w (G first when with_g) at the addresses tabs[0..nb)
 // (host vector, uploaded here); keys_le: this launch's keys as LE words on the
 // device; valid[key0 + j] written for key j of the launch.
 static int build_tables(Device& d, int w, const uint32_t* d_keys, uint32_t key0, uint32_t nb, int with_g,
                         uint32_t* valid, const std::vector<void*>& tabs) {
+  auto t0 = std::chrono::steady_clock::now();
   const pbftv::TableScratchSizes z = pbftv::table_scratch_sizes(w, nb);
-  DevBuf bases, lbuf, hbuf, ssc, esc, dtabs;
-  HIP_TRY(bases.ensure(z.bases));
-  HIP_TRY(lbuf.ensure(z.lbuf));
-  HIP_TRY(hbuf.ensure(z.hbuf));
-  HIP_TRY(ssc.ensure(z.small_scratch));
-  HIP_TRY(esc.ensure(z.entry_scratch));
-  HIP_TRY(dtabs.ensure(tabs.size() * sizeof(void*)));
-  HIP_TRY(hipMemcpyAsync(dtabs.p, tabs.data(), tabs.size() * sizeof(void*), hipMemcpyHostToDevice, d.stream));
-  pbftv::TableScratch sc{bases.p, lbuf.p, hbuf.p, ssc.p, esc.p, z.entry_lanes};
-  HIP_TRY(pbftv::launch_build_tables(w, d_keys, key0, nb, with_g, valid, dtabs.as<uint32_t* const>(), sc, d.stream));
+  // grow-only scratch kept by the device: a freed multi-GB buffer is wiped by
+  // the driver before its HBM can be handed out again, which costs more than
+  // the build
+  DevBuf* t = d.tab_scratch;
+  HIP_TRY(t[0].ensure(z.bases));
+  HIP_TRY(t[1].ensure(z.lbuf));
+  HIP_TRY(t[2].ensure(z.hbuf));
+  HIP_TRY(t[3].ensure(z.small_scratch));
+  HIP_TRY(t[4].ensure(z.entry_scratch));
+  HIP_TRY(t[5].ensure(tabs.size() * sizeof(void*)));
+  HIP_TRY(hipMemcpyAsync(t[5].p, tabs.data(), tabs.size() * sizeof(void*), hipMemcpyHostToDevice, d.stream));
+  trace("table scratch", d.id, t0);
+  pbftv::TableScratch sc{t[0].p, t[1].p, t[2].p, t[3].p, t[4].p, z.entry_lanes};
+  HIP_TRY(pbftv::launch_build_tables(w, d_keys, key0, nb, with_g, valid, t[5].as<uint32_t* const>(), sc, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
+  trace("table kernels", d.id, t0);
   return PBFTV_OK;
 }
 
@@ -853,11 +880,15 @@ static std::vector<uint32_t> keys_to_le(const uint8_t* pub_xy, uint32_t k) {
 // device pointer array.  valid_out (host, k entries) gets the key check.
 static int build_key_tables(Device& d, const std::vector<uint32_t>& le, uint32_t key0, uint32_t k,
                             uint32_t* valid_out) {
-  const uint32_t total = std::max<uint32_t>((uint32_t)d.qtab.size(), key0 + k);
-  while (d.qtab.size() < total) {
-    d.qtab.push_back(std::make_unique<DevBuf>());
-    HIP_TRY(d.qtab.back()->ensure(pbftv::table_bytes(d.qbits)));
+  auto t0 = std::chrono::steady_clock::now();
+  const uint32_t total = std::max<uint32_t>(d.nkeys, key0 + k);
+  if (d.qtab.size() < total) {  // one block for every table still missing
+    const size_t tb = pbftv::table_bytes(d.qbits), more = total - d.qtab.size();
+    d.qblocks.push_back(std::make_unique<DevBuf>());
+    HIP_TRY(d.qblocks.back()->ensure(more * tb));
+    for (size_t j = 0; j < more; ++j) d.qtab.push_back(d.qblocks.back()->as<uint8_t>() + j * tb);
   }
+  trace("key table allocation", d.id, t0);
   // key_valid grows with the key count (old flags kept)
   if (d.key_valid.cap < (size_t)total * 4) {
     DevBuf nv;
@@ -868,7 +899,7 @@ static int build_key_tables(Device& d, const std::vector<uint32_t>& le, uint32_t
     std::swap(d.key_valid.cap, nv.cap);
   }
   std::vector<void*> tabs(k);
-  for (uint32_t j = 0; j < k; ++j) tabs[j] = d.qtab[key0 + j]->p;
+  for (uint32_t j = 0; j < k; ++j) tabs[j] = d.qtab[key0 + j];
   DevBuf keys;
   HIP_TRY(keys.ensure((size_t)k * 64 + 64));
   HIP_TRY(hipMemcpyAsync(keys.p, le.data(), (size_t)k * 64, hipMemcpyHostToDevice, d.stream));
@@ -876,8 +907,9 @@ static int build_key_tables(Device& d, const std::vector<uint32_t>& le, uint32_t
     int rc = build_tables(d, d.qbits, keys.as<uint32_t>(), key0, k, 0, d.key_valid.as<uint32_t>(), tabs);
     if (rc != PBFTV_OK) return rc;
   }
+  trace("key table build", d.id, t0);
   std::vector<void*> ptrs(total);
-  for (uint32_t j = 0; j < total; ++j) ptrs[j] = d.qtab[j]->p;
+  for (uint32_t j = 0; j < total; ++j) ptrs[j] = d.qtab[j];
   HIP_TRY(d.qptrs.ensure((size_t)std::max<uint32_t>(total, 1) * sizeof(void*)));
   if (total)
     HIP_TRY(hipMemcpyAsync(d.qptrs.p, ptrs.data(), total * sizeof(void*), hipMemcpyHostToDevice, d.stream));
@@ -927,22 +959,44 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
+    auto t0 = std::chrono::steady_clock::now();
     d.have_keys = false;
     HIP_TRY(hipStreamSynchronize(d.stream));
-    for (auto& t : d.qtab) t->release();  // the old key tables go first: their HBM counts for the new ones
-    d.qtab.clear();
-    d.nkeys = 0;
-    size_t free_b = 0, total_b = 0;
+    size_t free_b = 0, total_b = 0, held = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    for (auto& b : d.qblocks) held += b->cap;  // the old key tables' HBM counts for the new ones
     int wg, wq;
-    choose_bits(k, free_b + d.gtab.cap, &wg, &wq);
-    if (d.gbits != wg) {  // G table: once per context (and width)
-      d.gtab.release();
-      HIP_TRY(d.gtab.ensure(pbftv::table_bytes(wg)));
-      DevBuf dummy;
-      HIP_TRY(dummy.ensure(64));
-      const int r = build_tables(d, wg, nullptr, 0, 1, 1, dummy.as<uint32_t>(), {d.gtab.p});
-      if (r != PBFTV_OK) return r;
+    const int dev_id = d.id;
+    choose_bits(k, free_b + held, &wg, &wq, [&](int g) {
+      std::lock_guard<std::mutex> gl(g_tables_mu);
+      auto it = g_tables.find({dev_id, g});
+      return it != g_tables.end() && !it->second.expired();  // ours or another context's: no new HBM
+    });
+    d.nkeys = 0;
+    if (wq != d.qbits || d.qtab.size() < k) {  // new width or too few slots: new blocks (freeing HBM
+      for (auto& b : d.qblocks) b->release();  // the driver wipes is slow: same-width re-registrations
+      d.qblocks.clear();                       // reuse their slots)
+      d.qtab.clear();
+    }
+    trace("release old key tables", d.id, t0);
+    if (d.gbits != wg || !d.gtab) {  // G table: once per GPU and width while any context holds it
+      d.gtab.reset();
+      d.gbits = 0;
+      std::lock_guard<std::mutex> gl(g_tables_mu);
+      auto& slot = g_tables[{d.id, wg}];
+      d.gtab = slot.lock();
+      if (!d.gtab) {
+        auto t = std::make_shared<DevBuf>();
+        HIP_TRY(t->ensure(pbftv::table_bytes(wg)));
+        DevBuf dummy;
+        HIP_TRY(dummy.ensure(64));
+        trace("G table allocation", d.id, t0);
+        const int r = build_tables(d, wg, nullptr, 0, 1, 1, dummy.as<uint32_t>(), {t->p});
+        if (r != PBFTV_OK) return r;
+        trace("G table build", d.id, t0);
+        slot = t;
+        d.gtab = std::move(t);
+      }
       d.gbits = wg;
     }
     d.qbits = wq;
@@ -1009,7 +1063,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   if (n <= pbftv::wave_path_max()) {
     HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, st, [&] {
       return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(),
-                                      d.nkeys, d.gtab.as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), d_bitmap, nullptr, st);
+                                      d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), d_bitmap, nullptr, st);
     }));
     return PBFTV_OK;
   }
@@ -1028,7 +1082,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
                                        d.prefix.p, pos, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
-    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.rec.p, n, d.gtab.as<uint32_t>(), d.qptrs.as<const uint32_t* const>(),
+    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.rec.p, n, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(),
                                     d_bitmap, sorted ? d.okb.as<uint8_t>() : nullptr, st);
   }));
   if (sorted) HIP_TRY(pbftv::launch_pack_bits(d.okb.as<uint8_t>(), n, d_bitmap, st));
@@ -1128,7 +1182,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     std::memset(st8 + oo, 0xFF, n);
     HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
       return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, st8 + oh, st8 + os, reinterpret_cast<uint32_t*>(st8 + ok), n,
-                                      d.key_valid.as<uint32_t>(), d.nkeys, d.gtab.as<uint32_t>(),
+                                      d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
                                       d.qptrs.as<const uint32_t* const>(), nullptr, st8 + oo, d.stream);
     }));
     // every wave writes its byte after its last read of the inputs, so once
