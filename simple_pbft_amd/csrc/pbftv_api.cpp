@@ -195,14 +195,32 @@ void par_copy(CopyPool* pool, void* dst, const void* src, size_t bytes) {
   });
 }
 
-bool is_pinned(const void* p) {
+// The device-side address of page-locked host memory p (hipHostMalloc'd or
+// hipHostRegister'ed), or nullptr for pageable memory.
+const uint8_t* pinned_dev_ptr(const void* p) {
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
-    return false;
+    return nullptr;
   }
-  return a.type == hipMemoryTypeHost;
+  if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+  return static_cast<const uint8_t*>(a.devicePointer) +
+         (static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(a.hostPointer));
 }
+
+bool is_pinned(const void* p) { return pinned_dev_ptr(p) != nullptr; }
+
+// Device scratch of one lane-path verify (stage-1 records, prefix products of
+// the batched inversion, key order, per-signature result bytes).
+struct VerifyScratch {
+  DevBuf rec, prefix, ksort, okb;
+  void release() {
+    rec.release();
+    prefix.release();
+    ksort.release();
+    okb.release();
+  }
+};
 
 struct Device {
   int id = -1;
@@ -221,15 +239,16 @@ struct Device {
   uint32_t nkeys = 0;
   bool have_keys = false;
   // ecdsa scratch
-  DevBuf hashes, sigs, key_idx, rec, prefix, bitmap;
-  DevBuf ksort, okb;  // key order of the lane path (perm + counts) and its per-signature results
+  DevBuf hashes, sigs, key_idx, bitmap;
+  VerifyScratch vs;  // the lane path's stage-1 records, prefix products, key order, result bytes
   HostBuf stage;  // zero-copy inputs/outputs of the small-batch path
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
-  hipStream_t cstream = nullptr;
-  HostBuf pin[2];
-  DevBuf din[2];
-  hipEvent_t h2d_ev[2] = {nullptr, nullptr}, comp_ev[2] = {nullptr, nullptr};
+  static constexpr int kSlots = 16;  // chunks staged ahead at most (PBFTV_HOST_SLOTS, default 16)
+  hipStream_t cstream = nullptr;     // the copies, in chunk order (one DMA queue keeps the link busy)
+  HostBuf pin[kSlots];
+  DevBuf din[kSlots];
+  hipEvent_t h2d_ev[kSlots] = {}, comp_ev[kSlots] = {};
   // sha scratch
   DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
   // message batches (Go-JSON on the device): packed column inputs, verifyMsg bytes,
@@ -578,21 +597,22 @@ void pbftv_close(pbftv_ctx* ctx) {
     for (auto& b : d->qblocks) b->release();
     for (auto& b : d->tab_scratch) b.release();
     d->gtab.reset();
-    for (DevBuf* b : {&d->qptrs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx, &d->rec,
-                      &d->prefix, &d->bitmap, &d->ksort, &d->okb, &d->data, &d->offsets, &d->lengths, &d->order,
+    d->vs.release();
+    for (DevBuf* b : {&d->qptrs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx,
+                      &d->bitmap, &d->data, &d->offsets, &d->lengths, &d->order,
                       &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok})
       b->release();  // explicit, with this device current (the destructors are a backstop)
     for (HostBuf* b : {&d->stage, &d->mstage, &d->mout}) b->release();
     if (d->scratch_ev) (void)hipEventDestroy(d->scratch_ev);
-    for (int k = 0; k < 2; ++k) {
+    if (d->cstream) {
+      (void)hipStreamSynchronize(d->cstream);
+      (void)hipStreamDestroy(d->cstream);
+    }
+    for (int k = 0; k < Device::kSlots; ++k) {
       d->pin[k].release();
       d->din[k].release();
       if (d->h2d_ev[k]) (void)hipEventDestroy(d->h2d_ev[k]);
       if (d->comp_ev[k]) (void)hipEventDestroy(d->comp_ev[k]);
-    }
-    if (d->cstream) {
-      (void)hipStreamSynchronize(d->cstream);
-      (void)hipStreamDestroy(d->cstream);
     }
     (void)hipStreamDestroy(d->stream);
   }
@@ -612,11 +632,11 @@ int pbftv_reserve(pbftv_ctx* ctx, uint64_t n) {
     Device& d = *dp;
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    HIP_TRY(d.rec.ensure(pbftv::ecdsa_record_bytes(n)));
-    HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
+    HIP_TRY(d.vs.rec.ensure(pbftv::ecdsa_record_bytes(n)));
+    HIP_TRY(d.vs.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
     if (pbftv::key_sort_wanted(n, d.nkeys)) {
-      HIP_TRY(d.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
-      HIP_TRY(d.okb.ensure(n));
+      HIP_TRY(d.vs.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
+      HIP_TRY(d.vs.okb.ensure(n));
     }
   }
   return PBFTV_OK;
@@ -1057,8 +1077,11 @@ int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uin
 }
 
 // ---------------------------------------------------------------- ecdsa
+// Lane path (or the one-wave-per-signature path for small n) of one batch on
+// stream st.  own == nullptr: the device's shared scratch, ordered across
+// streams by the scratch event; else the caller's (a pipeline stream's own).
 static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d_sigs, const uint32_t* d_key_idx,
-                            uint64_t n, uint8_t* d_bitmap, hipStream_t st) {
+                            uint64_t n, uint8_t* d_bitmap, hipStream_t st, VerifyScratch* own = nullptr) {
   if (!d.have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
   if (n <= pbftv::wave_path_max()) {
     HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, st, [&] {
@@ -1067,47 +1090,69 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
     }));
     return PBFTV_OK;
   }
-  HIP_TRY(d.rec.ensure(pbftv::ecdsa_record_bytes(n)));
-  HIP_TRY(d.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
-  HIP_TRY(scratch_acquire(d, st));
+  VerifyScratch& sc = own ? *own : d.vs;
+  HIP_TRY(sc.rec.ensure(pbftv::ecdsa_record_bytes(n)));
+  HIP_TRY(sc.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
+  if (!own) HIP_TRY(scratch_acquire(d, st));
   const bool sorted = pbftv::key_sort_wanted(n, d.nkeys);
   if (sorted) {  // comb lanes in key order: a wave's table lookups share keys (p256_kernels.hip k_key_*)
-    HIP_TRY(d.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
-    HIP_TRY(d.okb.ensure(n));
-    HIP_TRY(pbftv::launch_key_sort(d_key_idx, n, d.nkeys, d.ksort.p, st));
+    HIP_TRY(sc.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
+    HIP_TRY(sc.okb.ensure(n));
+    HIP_TRY(pbftv::launch_key_sort(d_key_idx, n, d.nkeys, sc.ksort.p, st));
   }
-  const uint32_t* pos = sorted ? d.ksort.as<uint32_t>() : nullptr;
+  const uint32_t* pos = sorted ? sc.ksort.as<uint32_t>() : nullptr;
   HIP_TRY(timed(d, PBFTV_K_ECDSA_SCALARS, st, [&] {
-    return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, d.rec.p,
-                                       d.prefix.p, pos, st);
+    return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, sc.rec.p,
+                                       sc.prefix.p, pos, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
-    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, d.rec.p, n, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(),
-                                    d_bitmap, sorted ? d.okb.as<uint8_t>() : nullptr, st);
+    return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, sc.rec.p, n, d.gtab->as<uint32_t>(),
+                                    d.qptrs.as<const uint32_t* const>(), d_bitmap, sorted ? sc.okb.as<uint8_t>() : nullptr,
+                                    st);
   }));
-  if (sorted) HIP_TRY(pbftv::launch_pack_bits(d.okb.as<uint8_t>(), n, d_bitmap, st));
-  HIP_TRY(scratch_release(d, st));
+  if (sorted) HIP_TRY(pbftv::launch_pack_bits(sc.okb.as<uint8_t>(), n, d_bitmap, st));
+  if (!own) HIP_TRY(scratch_release(d, st));
   return PBFTV_OK;
 }
 
-// Host-buffer verify of one shard, pipelined in chunks over two slots: while
-// chunk k runs on d.stream, chunk k+1 is staged (parallel memcpy into pinned
-// memory, skipped when the caller's buffers are pinned) and DMA'd on
-// d.cstream.  The bitmap comes back in one copy at the end.  Chunk sizes are
-// multiples of 512 (bitmap bytes and waves stay aligned).
-static uint64_t host_chunk(uint64_t m) {
+// Host-buffer verify of one shard, pipelined in chunks: the copies of every
+// chunk are queued back to back on one copy stream (each into its own device
+// slot, up to PBFTV_HOST_SLOTS = 16 ahead, so the PCIe link never waits for
+// a slot to be verified), and chunk k is verified on d.stream as soon as its
+// copy has landed.  Pageable inputs are staged by a parallel memcpy into
+// pinned slots first (skipped when the caller's buffers are pinned).  The
+// bitmap comes back in one copy at the end.  Chunk sizes are multiples of 512
+// (bitmap bytes and waves stay aligned).
+static uint64_t host_chunk() {
   uint64_t c = 262144;
   if (const char* e = getenv("PBFTV_HOST_CHUNK")) c = std::max<uint64_t>(512, strtoull(e, nullptr, 10));
-  c = (c + 511) / 512 * 512;
-  return std::min(c, (m + 511) / 512 * 512);
+  return (c + 511) / 512 * 512;
+}
+
+// Chunk sizes for m items: whole chunks and the remainder (a halving tail that
+// shortens the last, unhidden verify measured slower: more DMA commands, each
+// with a ~10-20 us gap on the copy engine; tools/host_path_ab.py).
+static std::vector<uint64_t> host_chunks(uint64_t m) {
+  const uint64_t c = host_chunk();
+  std::vector<uint64_t> out;
+  for (uint64_t r = m; r > 0; r -= std::min(c, r)) out.push_back(std::min(c, r));
+  return out;
+}
+
+static int host_slots() {
+  int s = Device::kSlots;
+  if (const char* e = getenv("PBFTV_HOST_SLOTS")) s = atoi(e);
+  return std::min(Device::kSlots, std::max(2, s));
 }
 
 static int verify_host_pipelined(Device& d, CopyPool* pool, const uint8_t* H, const uint8_t* S, const uint32_t* K,
                                  uint64_t m, uint8_t* out_bm) {
-  const uint64_t c = host_chunk(m), nch = (m + c - 1) / c;
+  const std::vector<uint64_t> chunks = host_chunks(m);
+  const uint64_t c = *std::max_element(chunks.begin(), chunks.end()), nch = chunks.size();
+  const int ns = (int)std::min<uint64_t>(nch, host_slots());
   const size_t oh = 0, os = 32 * c, ok = 96 * c, slot = 100 * c;  // slot layout: hashes | sigs | keys
   if (!d.cstream) HIP_TRY(hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking));
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < ns; ++k) {
     if (!d.h2d_ev[k]) HIP_TRY(hipEventCreateWithFlags(&d.h2d_ev[k], hipEventDisableTiming));
     if (!d.comp_ev[k]) HIP_TRY(hipEventCreateWithFlags(&d.comp_ev[k], hipEventDisableTiming));
     HIP_TRY(d.din[k].ensure(slot + 64));
@@ -1117,14 +1162,15 @@ static int verify_host_pipelined(Device& d, CopyPool* pool, const uint8_t* H, co
     }
   }
   HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
-  bool used[2] = {false, false};
-  for (uint64_t j = 0; j < nch; ++j) {
-    const int k = (int)(j & 1);
-    const uint64_t lo = j * c, cnt = std::min(c, m - lo);
+  bool used[Device::kSlots] = {};
+  uint64_t lo = 0;
+  for (uint64_t j = 0; j < nch; lo += chunks[j], ++j) {
+    const int k = (int)(j % ns);
+    const uint64_t cnt = chunks[j];
     uint8_t* dv = d.din[k].as<uint8_t>();
     if (used[k]) HIP_TRY(hipStreamWaitEvent(d.cstream, d.comp_ev[k], 0));  // slot's previous chunk verified
     if (pool) {
-      if (used[k]) HIP_TRY(hipEventSynchronize(d.h2d_ev[k]));            // its staging copy DMA'd
+      if (used[k]) HIP_TRY(hipEventSynchronize(d.h2d_ev[k]));             // its staging copy DMA'd
       uint8_t* pv = d.pin[k].as<uint8_t>();
       par_copy(pool, pv + oh, H + 32 * lo, 32 * cnt);
       par_copy(pool, pv + os, S + 64 * lo, 64 * cnt);

@@ -42,6 +42,37 @@ def build_consensus_test() -> str:
     return BIN
 
 
+CGO = os.path.join(CPP, "test_cgo_pattern")
+
+
+def build_cgo_pattern_test() -> str:
+    """tests/cpp/test_cgo_pattern.cpp: the C ABI driven as a cgo shim drives it."""
+    src = os.path.join(CPP, "test_cgo_pattern.cpp")
+    for so, d in ((LIB, "simple_pbft_amd"), (ORACLE, "oracle")):
+        if not os.path.exists(so):
+            subprocess.run(["make", "-C", os.path.join(ROOT, d), "-s", "-j8"], check=True)
+    if os.path.exists(CGO) and all(os.path.getmtime(s) <= os.path.getmtime(CGO) for s in (src, LIB, ORACLE)):
+        return CGO
+    subprocess.run(
+        ["g++", "-O1", "-std=c++17", "-Wall", "-o", CGO, src, "-L", os.path.dirname(LIB), "-lpbftv", "-L",
+         os.path.dirname(ORACLE), "-loracle", "-Wl,-rpath,$ORIGIN/../../simple_pbft_amd",
+         "-Wl,-rpath,$ORIGIN/../../oracle", "-lpthread"], check=True)
+    return CGO
+
+
+def test_cgo_pattern_program_builds():
+    assert os.path.exists(build_cgo_pattern_test())
+
+
+@pytest.mark.gpu
+def test_cgo_calling_pattern_gpu():
+    """Concurrent calls on one context from caller threads, caller-owned buffers
+    poisoned right after each return, every result vs the oracle."""
+    p = subprocess.run([build_cgo_pattern_test()], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert " 0 failed" in p.stdout
+
+
 def _run(mode: str, timeout: int):
     exe = build_consensus_test()
     p = subprocess.run([exe, mode], capture_output=True, text=True, timeout=timeout)
