@@ -83,9 +83,11 @@ INV_N_MACS = 25 * (36 + 54) + 162
 
 
 def macs_scalars(k: int) -> float:
-    """k signatures per lane share one inversion (Montgomery's trick, p256_kernels.hip)."""
+    """k signatures per lane, 64 k per wave share one inversion (Montgomery's trick per
+    lane and across the wave, p256_kernels.hip / wave_batch_inv_n): 7 products per
+    signature (4 at k = 1), 14 per lane for the wave scans, 1/(64 k) of an inversion."""
     per_sig = 7 if k > 1 else 4
-    return per_sig * FN_MUL + INV_N_MACS / k
+    return per_sig * FN_MUL + 14 * FN_MUL / k + INV_N_MACS / (64 * k)
 # v_mad_u64_u32 issue peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz (4-cycle wave64 issue);
 # measured 30.9 T lane-ops/s in profiles/r01_valu_microbench.txt
 MAD_PEAK = 256 * 4 * 16 * 2.4e9
@@ -97,7 +99,7 @@ def scalar_batch(n: int) -> int:
     if e in ("1", "2", "4", "8", "16"):
         return int(e)
     lanes, k = 256 * 4 * 64 * 2, 1
-    while k < 16 and n >= 2 * k * lanes:
+    while k < 4 and n >= 2 * k * lanes:
         k *= 2
     return k
 

@@ -345,10 +345,12 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
 // the wave -- and each record is written to the signature's position in key
 // order, pos[i] (k_key_scatter; identity without a key order): one full
 // 128-B line per lane, so the comb reads its lane's record coalesced and never
-// gathers through a permutation.  The K values of s share ONE inversion
-// (Montgomery's trick: prefix products c_j = s_0 ... s_j in a limb-major
-// scratch, inv = c_{K-1}^-1, then walking back w_j = inv * c_{j-1},
-// inv *= s_j): per signature 7 Montgomery multiplies + 1/K of a safegcd.
+// gathers through a permutation.  The 64 K values of s of a wave share ONE
+// inversion (Montgomery's trick twice: per lane, prefix products c_j = s_0 ...
+// s_j in a limb-major scratch; across the lanes, wave_batch_inv_n gives every
+// lane c_{K-1}^-1 from one lane-parallel safegcd; then walking back w_j = inv
+// * c_{j-1}, inv *= s_j): per signature 7 Montgomery multiplies + 14/K for the
+// wave scans + 1/(64 K) of an inversion.
 template <int K>
 __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict__ hashes,
                                                        const uint8_t* __restrict__ sigs,
@@ -380,7 +382,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     okm |= (ok ? 1u : 0u) << j;
   }
   fe inv;
-  fn_inv_mont_gcd(inv, acc);
+  wave_batch_inv_n(inv, acc);  // one inversion per wave (64 K signatures)
   for (int j = K - 1; j >= 0; --j) {
     const uint64_t i = lane + (uint64_t)j * L;
     const bool ok = (okm >> j) & 1u;
@@ -576,9 +578,12 @@ int scalar_batch(uint64_t n) {
     const int k = atoi(e);
     if (k == 1 || k == 2 || k == 4 || k == 8 || k == 16) return k;
   }
+  // with the inversion shared by the wave (wave_batch_inv_n), K only trades
+  // per-lane scan products against occupancy: K = 4 at 1M (0.134 ms; K = 2 /
+  // 8 / 16: 0.158 / 0.143 / 0.169 ms, tools/ab.sh same box)
   const uint64_t lanes = 256ull * 4 * 64 * 2;
   int k = 1;
-  while (k < 16 && n >= (uint64_t)(2 * k) * lanes) k *= 2;
+  while (k < 4 && n >= (uint64_t)(2 * k) * lanes) k *= 2;
   return k;
 }
 

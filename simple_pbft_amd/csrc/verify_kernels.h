@@ -726,6 +726,49 @@ __device__ __forceinline__ void inv_mod_n_wave(fe& D, const uint32_t x[8]) {
   }
 }
 
+// Montgomery's trick across the wave: inv = acc^-1 (Montgomery form mod n,
+// acc in Montgomery form and nonzero) for every lane with ONE inversion per
+// wave.  Prefix and suffix products over the lanes by shuffle scans (12
+// products per lane), inv_mod_n_wave of the total on the scalar unit, then
+// acc_l^-1 = (prefix_{l-1} suffix_{l+1}) total^-1 (2 products).  Every lane of
+// the wave must call it.
+__device__ __forceinline__ void shfl_fe(fe& d, const fe& s, int src_lane) {
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) d.v[l] = (uint32_t)__shfl((int)s.v[l], src_lane, 64);
+}
+
+__device__ __forceinline__ void wave_batch_inv_n(fe& inv, const fe& acc) {
+  const int lane = (int)(threadIdx.x & 63u);
+  fe one, pre = acc, suf = acc, a, b;
+  fe_set(one, kOneN);
+  PBFTV_UNROLL for (int k = 1; k < 64; k <<= 1) {
+    shfl_fe(a, pre, lane - k);
+    shfl_fe(b, suf, lane + k);
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+      a.v[l] = lane >= k ? a.v[l] : one.v[l];
+      b.v[l] = lane + k < 64 ? b.v[l] : one.v[l];
+    }
+    fn_mul(pre, pre, a);  // inclusive prefix product
+    fn_mul(suf, suf, b);  // inclusive suffix product
+  }
+  fe tot;
+  fn_canon(tot, pre);
+  uint32_t w[8];
+  fe_to_words(w, tot);
+  PBFTV_UNROLL for (int k = 0; k < 8; ++k) w[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 63);
+  fe D, r2n, invt;
+  inv_mod_n_wave(D, w);  // R / total: the plain inverse of the product of the (plain) values
+  fe_set(r2n, kR2N);
+  fn_mul(invt, D, r2n);  // its Montgomery form
+  shfl_fe(a, pre, lane - 1);
+  shfl_fe(b, suf, lane + 1);
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+    a.v[l] = lane >= 1 ? a.v[l] : one.v[l];
+    b.v[l] = lane < 63 ? b.v[l] : one.v[l];
+  }
+  fn_mul(a, a, b);
+  fn_mul(inv, a, invt);
+}
+
 // a b 2^-261 mod m with a per-lane modulus m (29-bit limbs) and mp = -m^-1 mod
 // 2^29: one step of the latency path runs mod-n and mod-p products side by
 // side on different lanes.  Inputs limbs < 2^29, a < 2^257, b < 2^261;
