@@ -36,6 +36,13 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// majority as ONE v_bitop3_b32 (0xE8: set when two or more inputs are set;
+// symmetric, so operand order is free); the compiler's xor + v_bfi_b32 form is
+// two instructions (64 per block)
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
 __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
   uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
@@ -54,7 +61,7 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = h + S1 + ch + kK256[r] + wr;
     const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-    const uint32_t mj = (a & b) | (c & (a | b));
+    const uint32_t mj = maj(a, b, c);
     const uint32_t t2 = S0 + mj;
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
