@@ -290,9 +290,11 @@ int pbftv_verify_msg_batch(int64_t state_view_id, int64_t state_last_seq, const 
 /* Register the replica public keys (k * 64 B, X||Y big-endian); replaces any
  * previous set.  out_valid[j] = 1 if key j is a valid P-256 point (0 <= X,Y < p
  * and on the curve); signatures naming an invalid key always fail.  Builds the
- * fixed-base comb tables on every device (one host thread per GPU): the G table
- * once per context and width, and one table allocation per key.  Geometry: see
- * pbftv_table_config. */
+ * fixed-base comb tables on every device (one host thread per GPU).  The G
+ * table is built once per GPU and width and shared by every context of the
+ * process on that GPU; the key tables of one call share one allocation, and a
+ * re-registration at the same width reuses it (no VRAM re-allocation).
+ * Geometry: see pbftv_table_config. */
 int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid);
 
 /* Incremental key changes (membership changes without a rebuild of every
