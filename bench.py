@@ -392,13 +392,40 @@ def _sha_run(ver, data, off, ln, steps, label):
     for b in (dd, do, dl, dord, dg):
         b.free()
     ops = blocks * SHA_OPS_PER_BLOCK
-    return {"workload": label.format(n=n, lens=lo_hi(ln), gb=total / 1e9, blocks=blocks),
+    cpu = openssl_sha256(data, off, ln, dig)
+    return {"workload": label.format(n=n, lens=lo_hi(ln), gb=total / 1e9, blocks=blocks), "cpu_baseline": cpu,
             "digests_per_s": n / best, "GB_per_s": total / best / 1e9, "ms": best * 1e3, "kernel_ms": kavg * 1e3,
             "roofline": {"bound": "valu", "achieved": ops / kavg / 1e12, "peak": VALU_PEAK / 1e12,
                          "unit": "T VALU ops/s (1528 per 64-B block, SURVEY §8(d))",
                          "frac": ops / kavg / VALU_PEAK, "hbm_GB_per_s": (total + 32 * n) / kavg / 1e9,
                          "hbm_frac": (total + 32 * n) / kavg / 8e12},
             "check": ok}
+
+
+def openssl_sha256(data, off, ln, gpu_digests):
+    """The same messages through OpenSSL 3 EVP_Digest SHA-256 (SHA-NI, like Go's
+    crypto/sha256 assembly) on 16 host threads (oracle/openssl_standin.c,
+    SURVEY.md §8(d)(ii)); best of 3, digests compared with the GPU's."""
+    so = os.path.join(ROOT, "oracle", "libopenssl_standin.so")
+    if not os.path.exists(so):
+        return None
+    L = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    L.standin_sha256_batch.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_int]
+    n = len(ln)
+    off64, ln32 = np.ascontiguousarray(off, np.uint64), np.ascontiguousarray(ln, np.uint32)
+    out = np.zeros((n, 32), np.uint8)
+    threads = min(16, os.cpu_count() or 1)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        L.standin_sha256_batch(data.ctypes.data, off64.ctypes.data, ln32.ctypes.data, n, out.ctypes.data, threads)
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    return {"value": n / t, "unit": "digests/s", "GB_per_s": float(ln32.sum()) / t / 1e9, "cores": threads,
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(), "kind": "openssl_standin",
+            "sample": f"all {n} messages (oracle/openssl_standin.c EVP_Digest, {threads} pthreads)",
+            "agrees_with_gpu": bool((out == gpu_digests).all())}
 
 
 def lo_hi(ln):
@@ -540,15 +567,16 @@ def main():
                            "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc else None}
         out["kernels"] = kern
         out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
-        out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "what": "pbftv_register_keys: G table + one table per key built on the device (incl. allocation)"}
+        out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "what": "pbftv_register_keys: G table + the key tables built on the device (incl. allocation)"}
         if not args.no_extras and ws == 1:
             out["host_path"] = host_path(ver, H, S, K, ok)
             out["host_path_verifies_per_s"] = out["host_path"]["pageable"]["verifies_per_s"]
-            p50_4, p99_4 = qc_latency(ver, 4, 3, 2000, 11)
-            p50_100, p99_100 = qc_latency(ver, 100, 67, 1000, 12)
+            p50_4, p99_4 = qc_latency(ver, 4, 3, 10000, 11)
+            p50_100, p99_100 = qc_latency(ver, 100, 67, 2000, 12)
             out["qc_latency_us"] = {"p50_n4_3sigs": p50_4, "p99_n4_3sigs": p99_4, "p50_n100_67sigs": p50_100,
-                                    "p99_n100_67sigs": p99_100,
-                                    "definition": "host submit -> accept bitmap + quorum on host, pbftv_qc_verify"}
+                                    "p99_n100_67sigs": p99_100, "calls": {"n4": 10000, "n100": 2000},
+                                    "definition": "host submit -> accept bitmap + quorum on host, pbftv_qc_verify, "
+                                                  "one certificate per call (SURVEY.md §8(d))"}
             sample = 262144
             cb = openssl_standin(pub, H, S, K, sample=sample)
             if cb is not None:
@@ -572,6 +600,11 @@ def main():
                 "config5": run_config5(ver),
                 "pbft_digests": run_sha_pbft(ver),
             }
+            # the same certificates inside large batches: device time per certificate
+            oc = out["other_configs"]
+            out["qc_latency_us"]["in_batch_us_per_cert"] = {
+                "n4_3sigs": oc["config2"]["ms"] * 1e3 / oc["config2"]["certs"],
+                "n100_67sigs": oc["config3"]["ms"] * 1e3 / oc["config3"]["certs"]}
         print(json.dumps(out), flush=True)
     for b in (dh, ds, dk, db):
         b.free()

@@ -321,12 +321,12 @@ int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uin
  * key_idx (n, index into the registered table).  out_bitmap: ceil(n/8) B.
  * Batches up to 2048 signatures take the one-launch latency path (inputs read
  * by the kernel straight from pinned memory).  Larger batches are split into
- * one shard per device and each shard is pipelined in chunks: staging copy
- * (parallel memcpy into pinned memory; skipped when all three input buffers
- * come from pbftv_host_alloc or are otherwise pinned) -> DMA (one copy stream,
- * chunks back to back into up to PBFTV_HOST_SLOTS = 16 device slots) -> verify
- * as each chunk lands (PBFTV_HOST_CHUNK, default 262144 signatures;
- * PBFTV_COPY_THREADS staging threads, default min(8, host threads - 1)). */
+ * one shard per device and each shard is pipelined in chunks: DMA of the
+ * caller's buffers as they are (pinned memory, e.g. from pbftv_host_alloc,
+ * directly; pageable memory through the runtime's staging) on one copy
+ * stream, chunks back to back into up to PBFTV_HOST_SLOTS = 16 device slots,
+ * each chunk verified as it lands (PBFTV_HOST_CHUNK, default 262144
+ * signatures; the last chunk PBFTV_HOST_LAST, default 65536). */
 int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs,
                                   const uint32_t* key_idx, uint64_t n, uint8_t* out_bitmap);
 

@@ -8,6 +8,9 @@
  * its own EC_KEY objects.  bench.py times it beside the GPU on the same
  * signatures and checks that the accept bits agree.
  *
+ * standin_sha256_batch is the same for utils.Hash (SURVEY.md §8(d)(ii):
+ * EVP_Digest SHA-256, SHA-NI on x86-64 like Go's crypto/sha256 assembly).
+ *
  * Semantics match Go crypto/ecdsa.Verify for 32-byte hashes: r, s outside
  * [1, n-1] are rejected by OpenSSL; keys that OpenSSL refuses to load
  * (off-curve, coordinate >= p) reject every signature naming them.
@@ -16,6 +19,7 @@
 #include <openssl/ec.h>
 #include <openssl/ecdsa.h>
 #include <openssl/err.h>
+#include <openssl/evp.h>
 #include <openssl/obj_mac.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -94,4 +98,38 @@ int64_t standin_ecdsa_p256_verify_batch(const uint8_t* hashes, const uint8_t* si
   free(th);
   free(jobs);
   return acc;
+}
+
+typedef struct {
+  const uint8_t* data;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
+  uint64_t lo, hi;
+  uint8_t* out;
+} sha_job_t;
+
+static void* sha_worker(void* arg) {
+  sha_job_t* j = (sha_job_t*)arg;
+  const EVP_MD* md = EVP_sha256();
+  for (uint64_t i = j->lo; i < j->hi; ++i)
+    EVP_Digest(j->data + j->offsets[i], j->lengths[i], j->out + 32 * i, NULL, md, NULL);
+  return NULL;
+}
+
+/* SHA-256 of n messages (data + offsets[i], lengths[i] bytes) on `threads`
+ * host threads into out (n * 32 B).  Returns 0, or -1 on allocation failure. */
+int standin_sha256_batch(const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
+                         uint8_t* out, int threads) {
+  if (threads < 1) threads = 1;
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  sha_job_t* jobs = (sha_job_t*)calloc((size_t)threads, sizeof(sha_job_t));
+  if (!th || !jobs) return -1;
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (sha_job_t){data, offsets, lengths, n * t / threads, n * (t + 1) / threads, out};
+    pthread_create(&th[t], NULL, sha_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+  return 0;
 }

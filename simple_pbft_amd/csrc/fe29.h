@@ -11,10 +11,10 @@
 //
 // Reduction mod p exploits p = 2^256 - 2^224 + 2^192 + 2^96 - 1 == -1 (mod 2^29):
 // the Montgomery quotient digit is m = t_i mod 2^29 (p' = 1) and m*p lands on
-// columns i+3, i+6, i+7, i+8 as m<<9, m<<18, -(m<<21), m<<24 -- four shifted
-// adds, no multiplies.  The one subtraction is made an addition of
-// (2^29-1-m)<<21; the surplus is cancelled by seeding the accumulator with
-// kMontBiasP = -K mod p (tools/gen_p256_consts.py).
+// columns i+3, i+6, i+7, i+8 as m<<9, m<<18, -(m<<21), m<<24.  The negative
+// term is folded into its neighbour: -m 2^224 + m 2^256 = m (2^29 - 2^21) in
+// column i+7 + m (2^24 - 1) in column i+8, so the digit step is four MADs by
+// positive SGPR constants (2^9, 2^18, kC21, kC24), no negation, no bias.
 //
 // Value/limb invariants (checked by tests/test_algo_cpu.py on CPU).  A Montgomery
 // product satisfies out < a*b/2^261 + p + 2^225, whose fixed point gives:
@@ -148,6 +148,10 @@ PBFTV_HD void fe_neg_lazy(fe& r, const fe& a) {
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = kP2Borrow[i] - a.v[i];
 }
 
+// digit-step multipliers for columns i+7 and i+8 (see the header)
+constexpr uint32_t kC21 = (1u << 29) - (1u << 21);
+constexpr uint32_t kC24 = (1u << 24) - 1u;
+
 // A power of two the compiler cannot see: on the device, m * opaque(2^k) + t
 // becomes ONE v_mad_u64_u32 (multiplier in an SGPR) instead of a 64-bit
 // shift plus v_lshl_add_u64 (whose shift field only reaches 4).
@@ -163,14 +167,14 @@ static inline uint32_t opaque_u32(uint32_t c) { return c; }
 
 // Montgomery reduction of the 17 column accumulators (t[17] is scratch).
 PBFTV_HD void fe_mont_reduce_p(fe& r, uint64_t t[18]) {
-  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
-                 c24 = opaque_u32(1u << 24);
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(kC21),
+                 c24 = opaque_u32(kC24);
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     const uint32_t m = (uint32_t)t[i] & kMask29;
     t[i + 1] += t[i] >> 29;
     t[i + 3] += (uint64_t)m * c9;
     t[i + 6] += (uint64_t)m * c18;
-    t[i + 7] += (uint64_t)(m ^ kMask29) * c21;
+    t[i + 7] += (uint64_t)m * c21;
     t[i + 8] += (uint64_t)m * c24;
   }
   PBFTV_UNROLL for (int j = 9; j < 16; ++j) {
@@ -187,7 +191,7 @@ PBFTV_HD void fe_mont_digit_p(uint64_t t[18], int i, uint32_t c9, uint32_t c18, 
   t[i + 1] += t[i] >> 29;
   t[i + 3] += (uint64_t)m * c9;
   t[i + 6] += (uint64_t)m * c18;
-  t[i + 7] += (uint64_t)(m ^ kMask29) * c21;
+  t[i + 7] += (uint64_t)m * c21;
   t[i + 8] += (uint64_t)m * c24;
 }
 
@@ -207,10 +211,10 @@ PBFTV_HD void fe_mont_out_p(fe& r, uint64_t t[18]) {
 // wave at 2 waves/SIMD).  Same sums in the same columns as
 // fe_mul_rows_then_reduce -- identical results.
 PBFTV_HD void fe_mul(fe& r, const fe& a, const fe& b) {
-  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
-                 c24 = opaque_u32(1u << 24);
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(kC21),
+                 c24 = opaque_u32(kC24);
   uint64_t t[18];
-  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = 0;
   PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * b.v[j];
@@ -223,10 +227,10 @@ PBFTV_HD void fe_mul(fe& r, const fe& a, const fe& b) {
 // ONE Montgomery reduction.  Column bound: a, b limbs < 2^29 and c < 2^30,
 // d < 2^29 give < 9 (2^58 + 2^59) < 2^62.8 before the reduction's additions.
 PBFTV_HD void fe_mul2_add(fe& r, const fe& a, const fe& b, const fe& c, const fe& d) {
-  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
-                 c24 = opaque_u32(1u << 24);
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(kC21),
+                 c24 = opaque_u32(kC24);
   uint64_t t[18];
-  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = 0;
   PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * b.v[j];
@@ -239,12 +243,12 @@ PBFTV_HD void fe_mul2_add(fe& r, const fe& a, const fe& b, const fe& c, const fe
 // fe_sqr with the reduction interleaved (after square row i columns <= 2i+1
 // are final); measured no faster than fe_sqr, kept for tools/fmul_bench.hip.
 PBFTV_HD void fe_sqr_il(fe& r, const fe& a) {
-  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(1u << 21),
-                 c24 = opaque_u32(1u << 24);
+  const uint32_t c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18), c21 = opaque_u32(kC21),
+                 c24 = opaque_u32(kC24);
   uint64_t t[18];
   uint32_t a2[9];
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) a2[i] = a.v[i] << 1;
-  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = 0;
   PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     t[2 * i] += (uint64_t)a.v[i] * a.v[i];
@@ -260,7 +264,7 @@ PBFTV_HD void fe_sqr_il(fe& r, const fe& a) {
 // interleaves the two and is ~10 % faster on gfx950)
 PBFTV_HD void fe_mul_rows_then_reduce(fe& r, const fe& a, const fe& b) {
   uint64_t t[18];
-  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = 0;
   PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += (uint64_t)a.v[i] * b.v[j];
@@ -273,7 +277,7 @@ PBFTV_HD void fe_sqr(fe& r, const fe& a) {
   uint64_t t[18];
   uint32_t a2[9];
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) a2[i] = a.v[i] << 1;
-  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = kMontBiasP[k];
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) t[k] = 0;
   PBFTV_UNROLL for (int k = 9; k < 18; ++k) t[k] = 0;
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
     t[2 * i] += (uint64_t)a.v[i] * a.v[i];

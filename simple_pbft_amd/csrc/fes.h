@@ -11,9 +11,10 @@
 //     hi32(t_i) * 8, ONE v_mad_i64_i32 -- no mask, no 64-bit shift + add
 //     (fe29.h: and + v_lshrrev_b64 + v_lshl_add_u64).  The top digit is kept at
 //     29 bits so the output stays below T / 2^261 + 1.0001 p;
-//   * the -m 2^224 term of m p is added as (~m) 2^21 into column i+7, whose
-//     constant surplus (2^32 - 1) 2^21 is pre-subtracted from the column
-//     (exact integer arithmetic: no bias mod p).
+//   * the -m 2^224 + m 2^256 terms of m p are added as m (2^29 - 2^21) into
+//     column i+7 and m (2^24 - 1) into column i+8 (the same integer:
+//     2^232 - 2^224 + 2^256 - 2^232): two MADs by positive constants, no
+//     negation of m and no bias in the columns.
 //
 // Types (checked by tests/test_algo_cpu.py, CPU harness):
 //   S (product output, fs_norm output): limbs 0..7 in [0, 2^29), limb 8 signed,
@@ -32,38 +33,22 @@ namespace pbftv {
 // a * b with both limbs taken as signed 32-bit (v_mad_i64_i32 on the device)
 PBFTV_HD uint64_t smul(uint32_t a, uint32_t b) { return (uint64_t)((int64_t)(int32_t)a * (int64_t)(int32_t)b); }
 
-// surplus of the (~m) 2^21 terms: (2^32 - 1) 2^21 per 32-bit digit (columns
-// 7..14), (2^29 - 1) 2^21 for the 29-bit top digit (column 15)
-constexpr uint64_t kFsBias32 = (uint64_t)(-(int64_t)(0xFFFFFFFFull << 21));
-constexpr uint64_t kFsBias29 = (uint64_t)(-(int64_t)((uint64_t)kMask29 << 21));
-
-// The bias as a value the compiler cannot fold: on the device an SGPR pair,
-// so it becomes the addend of the column's first v_mad (no separate 64-bit add).
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ uint64_t opaque_u64(uint64_t c) {
-  uint64_t r;
-  asm("s_mov_b64 %0, %1" : "=s"(r) : "s"(c));
-  return r;
-}
-#else
-static inline uint64_t opaque_u64(uint64_t c) { return c; }
-#endif
-
+// Column bound with the digit terms: products (<= 18 of |x| <= 2^58, or 9 of
+// 2^59) reach 2^62.2 in magnitude and the positive digit terms add < 2^61.1,
+// so every column stays inside int64 when its digit is taken.
 PBFTV_HD void fs_cols_init(uint64_t t[17]) {
-  const uint64_t b32 = opaque_u64(kFsBias32), b29 = opaque_u64(kFsBias29);
   PBFTV_UNROLL for (int k = 0; k < 17; ++k) t[k] = 0;
-  PBFTV_UNROLL for (int k = 7; k < 15; ++k) t[k] = b32;
-  t[15] = b29;
 }
 
 // Montgomery digit step of column i < 8 (32-bit digit, carry by one signed MAD)
+// (c21 = 2^29 - 2^21, c24 = 2^24 - 1: see the header)
 PBFTV_HD void fs_digit(uint64_t t[17], int i, uint32_t c8, uint32_t c9, uint32_t c18, uint32_t c21, uint32_t c24) {
   const uint32_t m = (uint32_t)t[i];
   const uint32_t h = (uint32_t)(t[i] >> 32);
   t[i + 1] += smul(h, c8);
   t[i + 3] += (uint64_t)m * c9;
   t[i + 6] += (uint64_t)m * c18;
-  t[i + 7] += (uint64_t)(~m) * c21;
+  t[i + 7] += (uint64_t)m * c21;
   t[i + 8] += (uint64_t)m * c24;
 }
 
@@ -73,23 +58,37 @@ PBFTV_HD void fs_digit_top(uint64_t t[17], uint32_t c9, uint32_t c18, uint32_t c
   t[9] += (uint64_t)((int64_t)t[8] >> 29);
   t[11] += (uint64_t)m * c9;
   t[14] += (uint64_t)m * c18;
-  t[15] += (uint64_t)(m ^ kMask29) * c21;
+  t[15] += (uint64_t)m * c21;
   t[16] += (uint64_t)m * c24;
 }
+
+// A limb whose bits the compiler must not know.  The masked limbs of fs_out
+// are provably non-negative; LLVM then rewrites a later smul's sign extension
+// as a zero extension and, seeing a signed x unsigned product, expands each
+// v_mad_i64_i32 into two v_mad_u64_u32, a sign shift and moves (the table
+// builder's loops were ~3x the MADs).  An empty asm hides the range.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t opaque_limb(uint32_t x) {
+  asm("" : "+v"(x));
+  return x;
+}
+#else
+static inline uint32_t opaque_limb(uint32_t x) { return x; }
+#endif
 
 // columns 9..16 -> S-type limbs (signed carries)
 PBFTV_HD void fs_out(fe& r, uint64_t t[17]) {
   PBFTV_UNROLL for (int j = 9; j < 16; ++j) {
-    r.v[j - 9] = (uint32_t)t[j] & kMask29;
+    r.v[j - 9] = opaque_limb((uint32_t)t[j] & kMask29);
     t[j + 1] += (uint64_t)((int64_t)t[j] >> 29);
   }
-  r.v[7] = (uint32_t)t[16] & kMask29;
+  r.v[7] = opaque_limb((uint32_t)t[16] & kMask29);
   r.v[8] = (uint32_t)((int64_t)t[16] >> 29);
 }
 
 #define PBFTV_FS_CONSTS                                                                                   \
   const uint32_t c8 = opaque_u32(8u), c9 = opaque_u32(1u << 9), c18 = opaque_u32(1u << 18),               \
-                 c21 = opaque_u32(1u << 21), c24 = opaque_u32(1u << 24)
+                 c21 = opaque_u32(kC21), c24 = opaque_u32(kC24)
 
 // r = a b 2^-261 (mod p), S-type.  Digit step i right after product row i
 // (column i is final then), as in fe_mul.

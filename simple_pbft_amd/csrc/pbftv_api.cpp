@@ -107,109 +107,6 @@ struct HostBuf {
   }
 };
 
-// Persistent host workers for the staging copies of the host-buffer path
-// (one parallel_for at a time; the caller's thread takes part).
-class CopyPool {
- public:
-  explicit CopyPool(int workers) {
-    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int size() const { return (int)th_.size() + 1; }
-  // fn(part) for part in [0, parts), spread over the workers and the caller
-  template <class F>
-  void parallel_for(int parts, F fn) {
-    std::lock_guard<std::mutex> one(run_mu_);
-    std::function<void(int)> f = fn;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      job_ = &f;
-      parts_ = parts;
-      next_ = 0;
-      done_ = 0;
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return done_ == parts_; });
-    job_ = nullptr;
-  }
-
- private:
-  void work() {
-    for (;;) {
-      int k;
-      std::function<void(int)>* f;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (!job_ || next_ >= parts_) return;
-        k = next_++;
-        f = job_;
-      }
-      (*f)(k);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (++done_ == parts_) done_cv_.notify_all();
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_ != nullptr); });
-        if (stop_) return;
-        seen = gen_;
-      }
-      work();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_, run_mu_;
-  std::condition_variable cv_, done_cv_;
-  std::function<void(int)>* job_ = nullptr;
-  int parts_ = 0, next_ = 0, done_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
-
-// parallel memcpy of one large block (pageable caller memory -> pinned staging)
-void par_copy(CopyPool* pool, void* dst, const void* src, size_t bytes) {
-  constexpr size_t kPiece = 1 << 20;
-  if (!pool || bytes < 2 * kPiece) {
-    std::memcpy(dst, src, bytes);
-    return;
-  }
-  const int parts = (int)std::min<size_t>((bytes + kPiece - 1) / kPiece, 4 * (size_t)pool->size());
-  const size_t per = (bytes + parts - 1) / parts;
-  pool->parallel_for(parts, [&](int k) {
-    const size_t lo = per * k, hi = std::min(bytes, lo + per);
-    if (hi > lo) std::memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, hi - lo);
-  });
-}
-
-// The device-side address of page-locked host memory p (hipHostMalloc'd or
-// hipHostRegister'ed), or nullptr for pageable memory.
-const uint8_t* pinned_dev_ptr(const void* p) {
-  hipPointerAttribute_t a;
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
-  return static_cast<const uint8_t*>(a.devicePointer) +
-         (static_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(a.hostPointer));
-}
-
-bool is_pinned(const void* p) { return pinned_dev_ptr(p) != nullptr; }
-
 // Device scratch of one lane-path verify (stage-1 records, prefix products of
 // the batched inversion, key order, per-signature result bytes).
 struct VerifyScratch {
@@ -246,7 +143,6 @@ struct Device {
   // path): two slots of pinned staging + device inputs, a copy stream
   static constexpr int kSlots = 16;  // chunks staged ahead at most (PBFTV_HOST_SLOTS, default 16)
   hipStream_t cstream = nullptr;     // the copies, in chunk order (one DMA queue keeps the link busy)
-  HostBuf pin[kSlots];
   DevBuf din[kSlots];
   hipEvent_t h2d_ev[kSlots] = {}, comp_ev[kSlots] = {};
   // sha scratch
@@ -328,22 +224,12 @@ std::map<std::pair<int, int>, std::weak_ptr<DevBuf>> g_tables;
 struct pbftv_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   bool timing = false;
-  std::unique_ptr<CopyPool> pool;  // staging copies of the host-buffer pipeline
 };
 
 namespace {
 
 constexpr uint64_t kShardAlign = 512;
 
-// staging-copy workers: PBFTV_COPY_THREADS, default min(8, host threads - 1)
-void ensure_pool(pbftv_ctx* ctx) {
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lk(mu);
-  if (ctx->pool) return;
-  int w = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()) - 1);
-  if (const char* e = getenv("PBFTV_COPY_THREADS")) w = std::max(0, atoi(e) - 1);
-  ctx->pool = std::make_unique<CopyPool>(w);
-}
 
 struct Shard {
   uint64_t lo, hi;
@@ -609,7 +495,6 @@ void pbftv_close(pbftv_ctx* ctx) {
       (void)hipStreamDestroy(d->cstream);
     }
     for (int k = 0; k < Device::kSlots; ++k) {
-      d->pin[k].release();
       d->din[k].release();
       if (d->h2d_ev[k]) (void)hipEventDestroy(d->h2d_ev[k]);
       if (d->comp_ev[k]) (void)hipEventDestroy(d->comp_ev[k]);
@@ -1119,8 +1004,9 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
 // chunk are queued back to back on one copy stream (each into its own device
 // slot, up to PBFTV_HOST_SLOTS = 16 ahead, so the PCIe link never waits for
 // a slot to be verified), and chunk k is verified on d.stream as soon as its
-// copy has landed.  Pageable inputs are staged by a parallel memcpy into
-// pinned slots first (skipped when the caller's buffers are pinned).  The
+// copy has landed.  The caller's buffers are DMA'd as they are: pinned memory
+// directly, pageable memory through the runtime's own staging (faster than a
+// parallel memcpy into pinned slots, profiles/r02_ab_host_path.jsonl).  The
 // bitmap comes back in one copy at the end.  Chunk sizes are multiples of 512
 // (bitmap bytes and waves stay aligned).
 static uint64_t host_chunk() {
@@ -1129,13 +1015,18 @@ static uint64_t host_chunk() {
   return (c + 511) / 512 * 512;
 }
 
-// Chunk sizes for m items: whole chunks and the remainder (a halving tail that
-// shortens the last, unhidden verify measured slower: more DMA commands, each
-// with a ~10-20 us gap on the copy engine; tools/host_path_ab.py).
+// Chunk sizes for m items: whole chunks, then a short last chunk (default
+// 65536, PBFTV_HOST_LAST), since the last chunk's verify is the one part no
+// copy hides.  (Halving every chunk of the tail measured slower: each DMA
+// command costs a ~10-20 us gap on the copy engine; tools/host_path_ab.py.)
 static std::vector<uint64_t> host_chunks(uint64_t m) {
   const uint64_t c = host_chunk();
+  uint64_t last = 65536;
+  if (const char* e = getenv("PBFTV_HOST_LAST")) last = strtoull(e, nullptr, 10) / 512 * 512;
+  if (last >= c || m <= c) last = 0;
   std::vector<uint64_t> out;
-  for (uint64_t r = m; r > 0; r -= std::min(c, r)) out.push_back(std::min(c, r));
+  for (uint64_t r = m - last; r > 0; r -= std::min(c, r)) out.push_back(std::min(c, r));
+  if (last) out.push_back(last);
   return out;
 }
 
@@ -1145,8 +1036,8 @@ static int host_slots() {
   return std::min(Device::kSlots, std::max(2, s));
 }
 
-static int verify_host_pipelined(Device& d, CopyPool* pool, const uint8_t* H, const uint8_t* S, const uint32_t* K,
-                                 uint64_t m, uint8_t* out_bm) {
+static int verify_host_pipelined(Device& d, const uint8_t* H, const uint8_t* S, const uint32_t* K, uint64_t m,
+                                 uint8_t* out_bm) {
   const std::vector<uint64_t> chunks = host_chunks(m);
   const uint64_t c = *std::max_element(chunks.begin(), chunks.end()), nch = chunks.size();
   const int ns = (int)std::min<uint64_t>(nch, host_slots());
@@ -1156,10 +1047,6 @@ static int verify_host_pipelined(Device& d, CopyPool* pool, const uint8_t* H, co
     if (!d.h2d_ev[k]) HIP_TRY(hipEventCreateWithFlags(&d.h2d_ev[k], hipEventDisableTiming));
     if (!d.comp_ev[k]) HIP_TRY(hipEventCreateWithFlags(&d.comp_ev[k], hipEventDisableTiming));
     HIP_TRY(d.din[k].ensure(slot + 64));
-    if (pool) {
-      d.pin[k].flags = hipHostMallocDefault;
-      HIP_TRY(d.pin[k].ensure(slot + 64));
-    }
   }
   HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
   bool used[Device::kSlots] = {};
@@ -1169,18 +1056,9 @@ static int verify_host_pipelined(Device& d, CopyPool* pool, const uint8_t* H, co
     const uint64_t cnt = chunks[j];
     uint8_t* dv = d.din[k].as<uint8_t>();
     if (used[k]) HIP_TRY(hipStreamWaitEvent(d.cstream, d.comp_ev[k], 0));  // slot's previous chunk verified
-    if (pool) {
-      if (used[k]) HIP_TRY(hipEventSynchronize(d.h2d_ev[k]));             // its staging copy DMA'd
-      uint8_t* pv = d.pin[k].as<uint8_t>();
-      par_copy(pool, pv + oh, H + 32 * lo, 32 * cnt);
-      par_copy(pool, pv + os, S + 64 * lo, 64 * cnt);
-      par_copy(pool, pv + ok, K + lo, 4 * cnt);
-      HIP_TRY(hipMemcpyAsync(dv, pv, ok + 4 * cnt, hipMemcpyHostToDevice, d.cstream));
-    } else {
-      HIP_TRY(hipMemcpyAsync(dv + oh, H + 32 * lo, 32 * cnt, hipMemcpyHostToDevice, d.cstream));
-      HIP_TRY(hipMemcpyAsync(dv + os, S + 64 * lo, 64 * cnt, hipMemcpyHostToDevice, d.cstream));
-      HIP_TRY(hipMemcpyAsync(dv + ok, K + lo, 4 * cnt, hipMemcpyHostToDevice, d.cstream));
-    }
+    HIP_TRY(hipMemcpyAsync(dv + oh, H + 32 * lo, 32 * cnt, hipMemcpyHostToDevice, d.cstream));
+    HIP_TRY(hipMemcpyAsync(dv + os, S + 64 * lo, 64 * cnt, hipMemcpyHostToDevice, d.cstream));
+    HIP_TRY(hipMemcpyAsync(dv + ok, K + lo, 4 * cnt, hipMemcpyHostToDevice, d.cstream));
     HIP_TRY(hipEventRecord(d.h2d_ev[k], d.cstream));
     HIP_TRY(hipStreamWaitEvent(d.stream, d.h2d_ev[k], 0));
     int rc = verify_on_device(d, dv + oh, dv + os, reinterpret_cast<const uint32_t*>(dv + ok), cnt,
@@ -1251,12 +1129,10 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((res[i] & 1u) << (i & 7));
     return PBFTV_OK;
   }
-  const bool pinned = is_pinned(hashes) && is_pinned(sig_rs) && is_pinned(key_idx);
-  if (!pinned) ensure_pool(ctx);
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    return verify_host_pipelined(d, pinned ? nullptr : ctx->pool.get(), hashes + 32 * s.lo, sig_rs + 64 * s.lo,
+    return verify_host_pipelined(d, hashes + 32 * s.lo, sig_rs + 64 * s.lo,
                                  key_idx + s.lo, s.hi - s.lo, out_bitmap + s.lo / 8);
   });
 }

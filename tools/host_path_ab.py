@@ -16,11 +16,14 @@ pub, H, S, K, ok = synth.config4(1 << 20, n_keys=100)
 ver = Verifier()
 ver.register_keys(pub)
 pins = [ver.pinned(a) for a in (H, S, K)]
+VARIANTS = [(262144, 0, 1), (262144, 65536, 1), (262144, 32768, 1), (262144, 0, 0), (262144, 65536, 0),
+            (131072, 32768, 0)]
 for rnd in range(2):
-    for chunk, tail in ((131072, 0), (131072, 1), (262144, 0), (262144, 1)):
+    for chunk, last, stage in VARIANTS:
         os.environ["PBFTV_HOST_CHUNK"] = str(chunk)
-        os.environ["PBFTV_HOST_TAIL"] = str(tail)
-        r = {"round": rnd, "chunk": chunk, "tail": tail}
+        os.environ["PBFTV_HOST_LAST"] = str(last)
+        os.environ["PBFTV_HOST_STAGE"] = str(stage)
+        r = {"round": rnd, "chunk": chunk, "last": last, "stage_pageable": stage}
         for label, arrays in (("pinned", tuple(p.a for p in pins)), ("pageable", (H, S, K))):
             got = ver.verify_batch(*arrays)
             ts = []
