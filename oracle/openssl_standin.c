@@ -108,11 +108,21 @@ typedef struct {
   uint8_t* out;
 } sha_job_t;
 
+/* One explicitly fetched SHA-256 and one digest context per thread: EVP_Digest
+ * with EVP_sha256() re-resolves the provider algorithm on every call under a
+ * process-wide lock (OpenSSL 3), which serialises the threads. */
 static void* sha_worker(void* arg) {
   sha_job_t* j = (sha_job_t*)arg;
-  const EVP_MD* md = EVP_sha256();
-  for (uint64_t i = j->lo; i < j->hi; ++i)
-    EVP_Digest(j->data + j->offsets[i], j->lengths[i], j->out + 32 * i, NULL, md, NULL);
+  EVP_MD* md = EVP_MD_fetch(NULL, "SHA256", NULL);
+  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  unsigned int len = 32;
+  for (uint64_t i = j->lo; i < j->hi; ++i) {
+    EVP_DigestInit_ex(c, md, NULL);
+    EVP_DigestUpdate(c, j->data + j->offsets[i], j->lengths[i]);
+    EVP_DigestFinal_ex(c, j->out + 32 * i, &len);
+  }
+  EVP_MD_CTX_free(c);
+  EVP_MD_free(md);
   return NULL;
 }
 

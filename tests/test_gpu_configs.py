@@ -1,0 +1,115 @@
+"""The SURVEY.md §8(d) configurations at full size as GPU parity tests (until
+round 2 they were checked only inside bench.py):
+
+  config 4  1,048,576 signatures over a 100-key table, 1 % corrupted evenly
+            over the 8 classes -- every class checked on its own, on the
+            device-resident path and on the host-buffer path (pageable and
+            pinned), and a sample plus every corrupted index against the oracle;
+  config 3  10,000 certificates of 67 signatures (n = 100, 2f + 1 = 67), 1 % of
+            the certificates carrying one bad vote: the quorum must fail
+            exactly there;
+  config 1  the 4-node, 1000-request pattern with every message signed,
+            through the four flushes (bench.run_config1's flow and check).
+
+Signatures come from OpenSSL (tools/synth.py), an implementation independent of
+both the product and the oracle.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import synth  # noqa: E402
+from simple_pbft_amd import Verifier  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+N4 = 1 << 20
+SEED = 0x50424654
+
+
+@pytest.fixture(scope="module")
+def ver():
+    v = Verifier(device_mask=1)
+    yield v
+    v.close()
+
+
+@pytest.fixture(scope="module")
+def cfg4():
+    return synth.config4(N4, n_keys=100, seed=SEED)
+
+
+def corruption_classes(n, frac=0.01, seed=SEED):
+    """index -> class (synth.corrupt draws the corrupted indices first, then
+    assigns class t % 8 to the t-th)."""
+    rng = np.random.default_rng(seed ^ 0x5A5A)
+    idx = rng.choice(n, int(round(n * frac)), replace=False)
+    return idx, np.arange(len(idx)) % 8
+
+
+def test_config4_full_size_every_class(ver, cfg4, oracle_lib):
+    pub, H, S, K, ok = cfg4
+    valid = ver.register_keys(pub)
+    assert valid.all()
+    dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
+    db = ver.alloc(0, (N4 + 7) // 8)
+    try:
+        ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, N4, db.ptr)
+        ver.sync(0)
+        got = np.unpackbits(db.to_host(), bitorder="little")[:N4].astype(bool)
+    finally:
+        for b in (dh, ds, dk, db):
+            b.free()
+    assert (got == ok).all(), f"{int((got != ok).sum())} signatures differ from the construction"
+    idx, cls = corruption_classes(N4)
+    for c, name in enumerate(synth.CLASSES):
+        sel = idx[cls == c]
+        assert len(sel) > 1000 and not got[sel].any(), name
+    # the oracle on every corrupted index and a sample of the rest
+    sample = np.unique(np.concatenate([idx, np.arange(0, N4, 97)]))
+    h, s, k = (np.ascontiguousarray(a[sample]) for a in (H, S, K))
+    bm = np.zeros((len(sample) + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(h.ctypes.data, s.ctypes.data, k.ctypes.data, len(sample),
+                                              pub.ctypes.data, len(pub), bm.ctypes.data, 16)
+    assert (np.unpackbits(bm, bitorder="little")[:len(sample)].astype(bool) == got[sample]).all()
+
+
+def test_config4_full_size_host_path(ver, cfg4):
+    pub, H, S, K, ok = cfg4
+    ver.register_keys(pub)
+    assert (ver.verify_batch(H, S, K) == ok).all()  # pageable (Go heap)
+    pins = [ver.pinned(a) for a in (H, S, K)]
+    assert (ver.verify_batch(*(p.a for p in pins)) == ok).all()
+
+
+def test_config3_full_size_quorum(ver):
+    per, n_certs, pool = 67, 10000, 500
+    pub, H, S, K = synth.certs(100, per, pool, seed=per * 7 + 100)
+    reps = n_certs // pool
+    H, S, K = np.tile(H, (reps, 1)), np.tile(S, (reps, 1)), np.tile(K, reps)
+    rng = np.random.default_rng(3)
+    bad_certs = rng.choice(n_certs, n_certs // 100, replace=False)
+    bad_sig = bad_certs * per + rng.integers(0, per, len(bad_certs))
+    S[bad_sig, 40] ^= 0x10  # one flipped bit of s in one vote of each bad certificate
+    ver.register_keys(pub)
+    got = ver.verify_batch(H, S, K).reshape(n_certs, per)
+    want = np.ones(n_certs * per, bool)
+    want[bad_sig] = False
+    assert (got.reshape(-1) == want).all()
+    quorum = got.sum(1) >= per  # 2f + 1 = 67 of n = 100
+    assert not quorum[bad_certs].any() and quorum.sum() == n_certs - len(bad_certs)
+
+
+def test_config1_every_message_signed(ver):
+    import bench
+    r = bench.run_config1(ver)
+    assert r["check"], r
+    assert "29000 signature checks" in r["workload"]
