@@ -58,10 +58,16 @@ hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const 
                              const uint32_t* const* qtabs,
                              uint8_t* bitmap, uint8_t* okb, hipStream_t st);
 // stage 0 (optional): key order pos[i] = position of signature i sorted by key
-// (scratch: key_sort_scratch_bytes, pos first).
+// (scratch: key_sort_scratch_bytes = a header of key_sort_header_bytes, which
+// must be ZERO when the scratch is first used and is left zero by every sort,
+// then pos).
 bool key_sort_wanted(uint64_t n, uint32_t nkeys);
+size_t key_sort_header_bytes();
 size_t key_sort_scratch_bytes(uint64_t n, uint32_t nkeys);
-hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, hipStream_t st);
+// parity: the caller's batch counter for this scratch (alternates the header's
+// two counter sets; any sequence of values that alternates is fine).
+hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, uint32_t parity,
+                           hipStream_t st);
 hipError_t launch_pack_bits(const uint8_t* okb, uint64_t n, uint8_t* bitmap, hipStream_t st);
 // latency path for small batches: one wave per signature (scalars, per-window
 // points, butterfly sum, check) in one launch.  Output: okbytes[i] (one byte per

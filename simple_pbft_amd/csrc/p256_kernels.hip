@@ -21,6 +21,7 @@ namespace pbftv {
 // key-order sort (k_key_*): blocks of the histogram/scatter passes, largest key count sorted
 constexpr uint32_t kSortBlocks = 256;
 constexpr uint32_t kSortMaxKeys = 1024;
+constexpr uint32_t kSortHdr = kSortMaxKeys + 64;  // key-sort header: 2 x (totals | claims), words each
 
 // ---------------------------------------------------------------------------
 // Table construction (p256_algo.h, "generic (W-bit) table construction"):
@@ -456,38 +457,58 @@ __device__ __forceinline__ void block_key_hist(uint32_t* h, const uint32_t* __re
   __syncthreads();
 }
 
+// Two launches, no memset, no scan launch, no fence.  The header holds two
+// sets of per-key counters (totals, claims); batch j counts into set j % 2
+// while k_key_hist's block 0 clears set (j + 1) % 2 for the next batch (that
+// set's last reader, the scatter of batch j - 1, finished before this launch
+// began).  Both sets start zeroed when the scratch is allocated.
+//   k_key_hist:    per-block histograms (LDS) added into total[];
+//   k_key_scatter: every block scans the <= 1025 totals in LDS itself (key
+//                  starts), claims its range of each key with one atomic on
+//                  claim[], and scatters through LDS cursors.
+// Round 2 had memset + hist + scan + scatter: 4 launches and two 5-us fills.
 __global__ void __launch_bounds__(256) k_key_hist(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
-                                                  uint32_t* __restrict__ total) {
+                                                  uint32_t* __restrict__ cur, uint32_t* __restrict__ other) {
   __shared__ uint32_t h[kSortMaxKeys + 1];
+  if (blockIdx.x == 0)
+    for (uint32_t b = threadIdx.x; b < 2 * kSortHdr; b += blockDim.x) other[b] = 0;
   block_key_hist(h, key_idx, n, nkeys);
   for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
-    if (h[b]) atomicAdd(&total[b], h[b]);
-}
-
-// exclusive scan of the m <= 2048 totals in place: one block, two per thread
-__global__ void __launch_bounds__(1024) k_key_scan(uint32_t* __restrict__ total, uint32_t m) {
-  __shared__ uint32_t s[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t a = 2 * t < m ? total[2 * t] : 0u, b = 2 * t + 1 < m ? total[2 * t + 1] : 0u;
-  s[t] = a + b;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    const uint32_t v = t >= off ? s[t - off] : 0u;
-    __syncthreads();
-    s[t] += v;
-    __syncthreads();
-  }
-  const uint32_t excl = s[t] - a - b;
-  if (2 * t < m) total[2 * t] = excl;
-  if (2 * t + 1 < m) total[2 * t + 1] = excl + a;
+    if (h[b]) atomicAdd(&cur[b], h[b]);
 }
 
 __global__ void __launch_bounds__(256) k_key_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
-                                                     uint32_t* __restrict__ start, uint32_t* __restrict__ pos) {
+                                                     const uint32_t* __restrict__ total, uint32_t* __restrict__ claim,
+                                                     uint32_t* __restrict__ pos) {
   __shared__ uint32_t h[kSortMaxKeys + 1];
-  block_key_hist(h, key_idx, n, nkeys);
+  __shared__ uint32_t start[kSortMaxKeys + 1];
+  __shared__ uint32_t part[256];
+  // key starts: exclusive scan of total[0..nkeys], thread t owns entries kPer t ..
+  constexpr uint32_t kPer = (kSortMaxKeys + 1 + 255) / 256;
+  const uint32_t t = threadIdx.x, m = nkeys + 1;
+  uint32_t v[kPer], sum = 0;
+  PBFTV_UNROLL for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t b = kPer * t + k;
+    v[k] = b < m ? total[b] : 0u;
+    sum += v[k];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    const uint32_t x = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  PBFTV_UNROLL for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t b = kPer * t + k;
+    if (b < m) start[b] = run;
+    run += v[k];
+  }
+  block_key_hist(h, key_idx, n, nkeys);  // (its first __syncthreads also publishes start[])
   for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
-    if (h[b]) h[b] = atomicAdd(&start[b], h[b]);  // this block's range of key b
+    if (h[b]) h[b] = start[b] + atomicAdd(&claim[b], h[b]);  // this block's range of key b
   __syncthreads();
   const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = (uint64_t)blockIdx.x * chunk;
   const uint64_t hi = lo + chunk < n ? lo + chunk : n;
@@ -521,18 +542,20 @@ bool key_sort_wanted(uint64_t n, uint32_t nkeys) {
   return nkeys > 8 && nkeys <= kSortMaxKeys && n >= 32768 && n < (1ull << 32);
 }
 
-size_t key_sort_scratch_bytes(uint64_t n, uint32_t nkeys) { return (size_t)n * 4 + (size_t)(nkeys + 1) * 4; }
+size_t key_sort_header_bytes() { return (size_t)(4 * kSortHdr) * 4; }
+size_t key_sort_scratch_bytes(uint64_t n, uint32_t) { return key_sort_header_bytes() + (size_t)n * 4; }
 
-hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, hipStream_t st) {
+hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, uint32_t parity,
+                           hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (nkeys > kSortMaxKeys) return hipErrorInvalidValue;
-  uint32_t* pos = reinterpret_cast<uint32_t*>(scratch);
-  uint32_t* total = pos + n;
-  hipError_t e = hipMemsetAsync(total, 0, (size_t)(nkeys + 1) * 4, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_key_hist, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, total);
-  hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(1024), 0, st, total, nkeys + 1);
-  hipLaunchKernelGGL(k_key_scatter, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, total, pos);
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* cur = hdr + (parity & 1u) * 2 * kSortHdr;  // totals | claims of this batch
+  uint32_t* other = hdr + (~parity & 1u) * 2 * kSortHdr;
+  uint32_t* pos = hdr + key_sort_header_bytes() / 4;
+  hipLaunchKernelGGL(k_key_hist, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, cur, other);
+  hipLaunchKernelGGL(k_key_scatter, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, cur, cur + kSortHdr,
+                     pos);
   return hipGetLastError();
 }
 
@@ -581,7 +604,9 @@ int scalar_batch(uint64_t n) {
   // with the inversion shared by the wave (wave_batch_inv_n), K only trades
   // per-lane scan products against occupancy: K = 4 at 1M (0.134 ms; K = 2 /
   // 8 / 16: 0.158 / 0.143 / 0.169 ms, tools/ab.sh same box)
-  const uint64_t lanes = 256ull * 4 * 64 * 2;
+  // K = 2 from 131072 (1M / 8, a strong-scaling shard: 0.046 vs 0.051 ms at
+  // K = 1, K = 4 0.056), K = 4 from 262144
+  const uint64_t lanes = 65536;
   int k = 1;
   while (k < 4 && n >= (uint64_t)(2 * k) * lanes) k *= 2;
   return k;

@@ -111,6 +111,7 @@ struct HostBuf {
 // the batched inversion, key order, per-signature result bytes).
 struct VerifyScratch {
   DevBuf rec, prefix, ksort, okb;
+  uint32_t sort_parity = 0;  // batches sorted with ksort (launch_key_sort's counter sets)
   void release() {
     rec.release();
     prefix.release();
@@ -157,6 +158,7 @@ struct Device {
   // different stream than the last scratch user first waits for it.
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_st = nullptr;
+  bool scratch_lazy = false;  // scratch_st == stream: scratch_ev not yet recorded for its last use
   // kernel timing (events recorded around launches while ctx timing is on)
   const bool* timing = nullptr;
   static constexpr int kKernels = 5;  // PBFTV_K_*
@@ -165,18 +167,46 @@ struct Device {
   uint64_t launches[kKernels] = {0, 0, 0, 0, 0};
 };
 
-// before / after enqueueing work that uses the device scratch on stream st
+// key-order scratch: a fresh allocation gets its header zeroed (the sort's
+// kernels leave it zero after every batch; p256_kernels.hip k_key_hist).
+// st == nullptr: a blocking memset.
+hipError_t ensure_key_sort(VerifyScratch& sc, uint64_t n, uint32_t nkeys, hipStream_t st) {
+  const size_t cap0 = sc.ksort.cap;
+  hipError_t e = sc.ksort.ensure(pbftv::key_sort_scratch_bytes(n, nkeys));
+  if (e != hipSuccess || sc.ksort.cap == cap0) return e;
+  return st ? hipMemsetAsync(sc.ksort.p, 0, pbftv::key_sort_header_bytes(), st)
+            : hipMemset(sc.ksort.p, 0, pbftv::key_sort_header_bytes());
+}
+
+// before / after enqueueing work that uses the device scratch on stream st.
+// A caller stream's use is fenced by an event recorded right after it.  The
+// library's own stream (d.stream, which lives as long as the context) is fenced
+// lazily: its event is recorded only when another stream next wants the
+// scratch -- recording later on the same stream covers at least the scratch
+// work -- so back-to-back calls on d.stream queue no marker between batches
+// (each marker costs the GPU a ~6 us gap between kernels, rocprof timeline).
 hipError_t scratch_acquire(Device& d, hipStream_t st) {
-  if (d.scratch_st != nullptr && d.scratch_st != st) return hipStreamWaitEvent(st, d.scratch_ev, 0);
-  return hipSuccess;
+  if (d.scratch_st == nullptr || d.scratch_st == st) return hipSuccess;
+  if (d.scratch_lazy) {
+    if (!d.scratch_ev) {
+      hipError_t e = hipEventCreateWithFlags(&d.scratch_ev, hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipEventRecord(d.scratch_ev, d.scratch_st);
+    if (e != hipSuccess) return e;
+    d.scratch_lazy = false;
+  }
+  return hipStreamWaitEvent(st, d.scratch_ev, 0);
 }
 
 hipError_t scratch_release(Device& d, hipStream_t st) {
+  d.scratch_st = st;
+  d.scratch_lazy = st == d.stream;
+  if (d.scratch_lazy) return hipSuccess;
   if (!d.scratch_ev) {
     hipError_t e = hipEventCreateWithFlags(&d.scratch_ev, hipEventDisableTiming);
     if (e != hipSuccess) return e;
   }
-  d.scratch_st = st;
   return hipEventRecord(d.scratch_ev, st);
 }
 
@@ -520,7 +550,7 @@ int pbftv_reserve(pbftv_ctx* ctx, uint64_t n) {
     HIP_TRY(d.vs.rec.ensure(pbftv::ecdsa_record_bytes(n)));
     HIP_TRY(d.vs.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
     if (pbftv::key_sort_wanted(n, d.nkeys)) {
-      HIP_TRY(d.vs.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
+      HIP_TRY(ensure_key_sort(d.vs, n, d.nkeys, nullptr));
       HIP_TRY(d.vs.okb.ensure(n));
     }
   }
@@ -980,20 +1010,20 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   HIP_TRY(sc.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
   if (!own) HIP_TRY(scratch_acquire(d, st));
   const bool sorted = pbftv::key_sort_wanted(n, d.nkeys);
-  if (sorted) {  // comb lanes in key order: a wave's table lookups share keys (p256_kernels.hip k_key_*)
-    HIP_TRY(sc.ksort.ensure(pbftv::key_sort_scratch_bytes(n, d.nkeys)));
-    HIP_TRY(sc.okb.ensure(n));
-    HIP_TRY(pbftv::launch_key_sort(d_key_idx, n, d.nkeys, sc.ksort.p, st));
+  if (sorted) {
+    HIP_TRY(sc.okb.ensure(n));  // comb lanes in key order: a wave's table lookups share keys (p256_kernels.hip k_key_*)
+    HIP_TRY(ensure_key_sort(sc, n, d.nkeys, st));
+    HIP_TRY(pbftv::launch_key_sort(d_key_idx, n, d.nkeys, sc.ksort.p, sc.sort_parity++, st));
   }
-  const uint32_t* pos = sorted ? sc.ksort.as<uint32_t>() : nullptr;
+  const uint32_t* pos = sorted ? sc.ksort.as<uint32_t>() + pbftv::key_sort_header_bytes() / 4 : nullptr;
   HIP_TRY(timed(d, PBFTV_K_ECDSA_SCALARS, st, [&] {
     return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, sc.rec.p,
                                        sc.prefix.p, pos, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
     return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, sc.rec.p, n, d.gtab->as<uint32_t>(),
-                                    d.qptrs.as<const uint32_t* const>(), d_bitmap, sorted ? sc.okb.as<uint8_t>() : nullptr,
-                                    st);
+                                    d.qptrs.as<const uint32_t* const>(), d_bitmap,
+                                    sorted ? sc.okb.as<uint8_t>() : nullptr, st);
   }));
   if (sorted) HIP_TRY(pbftv::launch_pack_bits(sc.okb.as<uint8_t>(), n, d_bitmap, st));
   if (!own) HIP_TRY(scratch_release(d, st));
