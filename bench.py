@@ -84,10 +84,13 @@ INV_N_MACS = 25 * (36 + 54) + 162
 
 def macs_scalars(k: int) -> float:
     """k signatures per lane, 64 k per wave share one inversion (Montgomery's trick per
-    lane and across the wave, p256_kernels.hip / wave_batch_inv_n): 7 products per
-    signature (4 at k = 1), 14 per lane for the wave scans, 1/(64 k) of an inversion."""
-    per_sig = 7 if k > 1 else 4
-    return per_sig * FN_MUL + 14 * FN_MUL / k + INV_N_MACS / (64 * k)
+    lane and across the wave over PLAIN s values, p256_kernels.hip k_ecdsa_scalars /
+    wave_batch_inv_n): per signature u1, u2 (2 products) + 3 (k - 1) / k for the
+    lane's prefix, back-substitution and running inverse; per lane 15 for the wave
+    scans and 2 (1 at k = 1) R-power fixes; 1/(64 k) of an inversion."""
+    per_sig = 2 + 3 * (k - 1) / k
+    per_lane = 15 + (2 if k > 1 else 1)
+    return per_sig * FN_MUL + per_lane * FN_MUL / k + INV_N_MACS / (64 * k)
 # v_mad_u64_u32 issue peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz (4-cycle wave64 issue);
 # measured 30.9 T lane-ops/s in profiles/r01_valu_microbench.txt
 MAD_PEAK = 256 * 4 * 16 * 2.4e9
@@ -459,7 +462,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--warmup-ms", type=float, default=100.0,
+                    help="keep warming up until this much wall time has passed (the comb's ~40 ms ramp after idle)")
     ap.add_argument("--n", type=int, default=1 << 20,
                     help="global batch (strong scaling, the default: BASELINE configs[3] shards N/k over k GPUs); "
                          "with --weak: signatures per rank")
@@ -505,11 +510,21 @@ def main():
         if n:
             ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
 
-    for _ in range(args.warmup):
-        step()
+    step()
     ver.sync(0)
     got = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
     check = bool((got == ok).all())
+    # Warm-up right before the timed steps, with no idle gap in between: after
+    # the GPU idles a few ms the comb needs ~40 ms of load to get back to its
+    # steady speed (first step after an 8 ms pause 1.37 ms, then 1.14, 1.24 ...
+    # 0.96 ms after 30 steps; rocprof trace profiles/r02_warm_ramp.txt).
+    t_w = time.perf_counter()
+    w = 0
+    while w < args.warmup or time.perf_counter() - t_w < args.warmup_ms * 1e-3:
+        step()
+        w += 1
+        if w % 8 == 0:
+            ver.sync(0)  # (the host clock follows the GPU)
 
     # wall clock over K steps, uninstrumented: a timing event between two
     # kernels costs the GPU a ~6 us gap (rocprof timeline, tools/rocpd_timeline.py)
@@ -540,7 +555,8 @@ def main():
     mode = "weak" if args.weak else "strong"
     out = {
         "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": ws, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3, "higher_is_better": True,
+        "warmup": args.warmup, "warmup_steps_run": w, "ms_per_step": t_max / args.steps * 1e3,
+        "higher_is_better": True,
         "scaling": mode, "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (OpenSSL-signed P-256 votes, tools/synth.py)",
         "config": {"workload": (f"config4: {n_global} ECDSA-P256 sigs" +

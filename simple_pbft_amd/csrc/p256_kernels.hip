@@ -350,8 +350,20 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
 // inversion (Montgomery's trick twice: per lane, prefix products c_j = s_0 ...
 // s_j in a limb-major scratch; across the lanes, wave_batch_inv_n gives every
 // lane c_{K-1}^-1 from one lane-parallel safegcd; then walking back w_j = inv
-// * c_{j-1}, inv *= s_j): per signature 7 Montgomery multiplies + 14/K for the
-// wave scans + 1/(64 K) of an inversion.
+// * c_{j-1}, inv *= s_j).
+//
+// The lane multiplies PLAIN s values (no conversion to Montgomery form per
+// signature) and fixes the powers of R once per lane.  With fn_mul(a, b) =
+// a b R^-1 mod n:
+//   forward   c_0 = s_0, c_j = fn_mul(c_{j-1}, s_j) = (s_0 .. s_j) R^-j;
+//             the lane total c_{K-1} = P R^(1-K) -> P R by one fn_mul with R^(K+1);
+//   wave      wave_batch_inv_n: P^-1 R, then one fn_mul with R^K: inv = P^-1 R^K;
+//   backward  invariant inv = (s_0 .. s_j)^-1 R^(j+1):
+//             w_j = fn_mul(inv, c_{j-1}) = s_j^-1 R (Montgomery form of s_j^-1),
+//             inv = fn_mul(inv, s_j); w_0 = inv.
+// Per signature 4 Montgomery multiplies (c_j, w_j, inv, and u1 / u2: 2) + 16/K
+// for the lane fixes and the wave scans + 1/(64 K) of an inversion (round 2
+// converted every s: 6 + 14/K).
 template <int K>
 __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict__ hashes,
                                                        const uint8_t* __restrict__ sigs,
@@ -359,11 +371,10 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
                                                        const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                        SigRec* __restrict__ rec, uint32_t* __restrict__ prefix,
                                                        const uint32_t* __restrict__ pos) {
+  static_assert(K >= 1 && K <= 16, "kRPowN covers R^0 .. R^17");
   const uint64_t L = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  fe r2n, acc;
-  fe_set(r2n, kR2N);
-  fe_set(acc, kOneN);
+  fe acc, rk;
   uint32_t okm = 0;
   for (int j = 0; j < K; ++j) {
     const uint64_t i = lane + (uint64_t)j * L;
@@ -374,16 +385,22 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
       ok = sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s);
       if (ok) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
     }
-    fe sv, sm;
+    fe sv;
     fe_from_words(sv, sw);
-    fn_mul(sm, sv, r2n);
-    fn_mul(acc, acc, sm);
-    if (K > 1)
+    if (j == 0) acc = sv;
+    else fn_mul(acc, acc, sv);
+    if (j + 1 < K)  // c_j is read back for w_{j+1}
       PBFTV_UNROLL for (int l = 0; l < 9; ++l) prefix[((uint64_t)j * 9 + l) * L + lane] = acc.v[l];
     okm |= (ok ? 1u : 0u) << j;
   }
+  fe_set(rk, kRPowN[K + 1]);
+  fn_mul(acc, acc, rk);        // P R: the lane total in Montgomery form
   fe inv;
-  wave_batch_inv_n(inv, acc);  // one inversion per wave (64 K signatures)
+  wave_batch_inv_n(inv, acc);  // P^-1 R: one inversion per wave (64 K signatures)
+  if (K > 1) {
+    fe_set(rk, kRPowN[K]);
+    fn_mul(inv, inv, rk);      // P^-1 R^K
+  }
   for (int j = K - 1; j >= 0; --j) {
     const uint64_t i = lane + (uint64_t)j * L;
     const bool ok = (okm >> j) & 1u;
@@ -396,11 +413,10 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     if (K > 1 && j > 0) {
       fe pre;
       PBFTV_UNROLL for (int l = 0; l < 9; ++l) pre.v[l] = prefix[((uint64_t)(j - 1) * 9 + l) * L + lane];
-      fn_mul(w, inv, pre);
-      fe sv, sm;
+      fn_mul(w, inv, pre);     // s_j^-1 R
+      fe sv;
       fe_from_words(sv, s);
-      fn_mul(sm, sv, r2n);
-      fn_mul(inv, inv, sm);
+      fn_mul(inv, inv, sv);    // (s_0 .. s_{j-1})^-1 R^j
     } else {
       w = inv;
     }

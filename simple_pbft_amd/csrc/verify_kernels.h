@@ -18,6 +18,10 @@
 
 namespace pbftv {
 
+#ifndef PBFTV_COMB_BLOCK
+#define PBFTV_COMB_BLOCK 256  // threads per k_ecdsa_comb block
+#endif
+
 #ifndef PBFTV_COMB_WAVES
 #define PBFTV_COMB_WAVES 4  // min waves per SIMD for k_ecdsa_comb: 128 VGPRs; +1.2 % over 2 (tools/ab.sh)
 #endif
@@ -172,7 +176,7 @@ __device__ __forceinline__ const uint4* entry_ptr(const uint4* __restrict__ tab,
 // Async copy of this lane's 64-B entry into sent[.][t]: four 16-B
 // global_load_lds, each writing the wave's 64 lanes contiguously at the
 // wave-uniform base &sent[k][t & ~63].
-__device__ __forceinline__ void issue_entry_lds(uint4 (*sent)[256], uint32_t t, const uint4* p) {
+__device__ __forceinline__ void issue_entry_lds(uint4 (*sent)[PBFTV_COMB_BLOCK], uint32_t t, const uint4* p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this lane's reads of the slot are done
   const uint32_t wb = t & ~63u;
   __builtin_amdgcn_global_load_lds(p + 0, &sent[0][wb], 16, 0, 0);
@@ -181,7 +185,7 @@ __device__ __forceinline__ void issue_entry_lds(uint4 (*sent)[256], uint32_t t, 
   __builtin_amdgcn_global_load_lds(p + 3, &sent[3][wb], 16, 0, 0);
 }
 
-__device__ __forceinline__ void read_entry_lds(uint4 (*sent)[256], uint32_t t, uint32_t ew[16]) {
+__device__ __forceinline__ void read_entry_lds(uint4 (*sent)[PBFTV_COMB_BLOCK], uint32_t t, uint32_t ew[16]) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies have landed
   uint4 e[4];
   PBFTV_UNROLL for (int k = 0; k < 4; ++k) e[k] = sent[k][t];
@@ -189,7 +193,7 @@ __device__ __forceinline__ void read_entry_lds(uint4 (*sent)[256], uint32_t t, u
 }
 
 template <int WG, int WQ>
-__global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigRec* __restrict__ rec, uint64_t n,
+__global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigRec* __restrict__ rec, uint64_t n,
                                                                     const uint4* __restrict__ gtab,
                                                                     const uint4* const* __restrict__ qtabs,
                                                                     uint8_t* __restrict__ bitmap,
@@ -197,10 +201,10 @@ __global__ void __launch_bounds__(256, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigR
   using S = CombSteps<WG, WQ>;
   // signed digits of u1 / u2 in step order, one column per thread: recoded once
   // in the prologue so the main loop holds no 256-bit digit shift registers
-  __shared__ typename S::Digit sdig[S::nD][256];
+  __shared__ typename S::Digit sdig[S::nD][PBFTV_COMB_BLOCK];
   // the table entry of the next step, streamed global -> LDS (no VGPRs held
   // while it is in flight): piece k of thread t at sent[k][t]
-  __shared__ uint4 sent[4][256];
+  __shared__ uint4 sent[4][PBFTV_COMB_BLOCK];
   const uint32_t t = threadIdx.x;
   // lane p reads record p: with a key order (k_key_*) the p-th signature by key,
   // written there by stage 1 (coalesced: no gather through a permutation)
@@ -918,8 +922,8 @@ void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* k
 template <int WG, int WQ>
 void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* const* qtabs, uint8_t* bitmap,
                    uint8_t* okb, hipStream_t st) {
-  const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL((k_ecdsa_comb<WG, WQ>), dim3((uint32_t)blocks), dim3(256), 0, st,
+  const uint64_t blocks = (n + PBFTV_COMB_BLOCK - 1) / PBFTV_COMB_BLOCK;
+  hipLaunchKernelGGL((k_ecdsa_comb<WG, WQ>), dim3((uint32_t)blocks), dim3(PBFTV_COMB_BLOCK), 0, st,
                      reinterpret_cast<const SigRec*>(rec), n, reinterpret_cast<const uint4*>(gtab),
                      reinterpret_cast<const uint4* const*>(qtabs), bitmap, okb);
 }
