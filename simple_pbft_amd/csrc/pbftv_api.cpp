@@ -144,7 +144,10 @@ struct Device {
   // path): two slots of pinned staging + device inputs, a copy stream
   static constexpr int kSlots = 16;  // chunks staged ahead at most (PBFTV_HOST_SLOTS, default 16)
   hipStream_t cstream = nullptr;     // the copies, in chunk order (one DMA queue keeps the link busy)
-  DevBuf din[kSlots];
+  hipStream_t stream2 = nullptr;     // the odd chunks' verifies (their own scratch vs2), so two chunks can overlap
+  VerifyScratch vs2;
+  hipEvent_t join_ev = nullptr;
+  DevBuf din[kSlots], keys_all;
   hipEvent_t h2d_ev[kSlots] = {}, comp_ev[kSlots] = {};
   // sha scratch
   DevBuf data, offsets, lengths, order, order_scratch, digests, expected, shabits;
@@ -520,6 +523,13 @@ void pbftv_close(pbftv_ctx* ctx) {
       b->release();  // explicit, with this device current (the destructors are a backstop)
     for (HostBuf* b : {&d->stage, &d->mstage, &d->mout}) b->release();
     if (d->scratch_ev) (void)hipEventDestroy(d->scratch_ev);
+    if (d->stream2) {
+      (void)hipStreamSynchronize(d->stream2);
+      (void)hipStreamDestroy(d->stream2);
+    }
+    d->vs2.release();
+    if (d->join_ev) (void)hipEventDestroy(d->join_ev);
+    d->keys_all.release();
     if (d->cstream) {
       (void)hipStreamSynchronize(d->cstream);
       (void)hipStreamDestroy(d->cstream);
@@ -1033,12 +1043,18 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
 // Host-buffer verify of one shard, pipelined in chunks: the copies of every
 // chunk are queued back to back on one copy stream (each into its own device
 // slot, up to PBFTV_HOST_SLOTS = 16 ahead, so the PCIe link never waits for
-// a slot to be verified), and chunk k is verified on d.stream as soon as its
-// copy has landed.  The caller's buffers are DMA'd as they are: pinned memory
+// a slot to be verified), and chunk k is verified as soon as its copy has
+// landed: even chunks on d.stream, odd chunks on d.stream2 with their own
+// scratch (so two chunks' verifies can overlap at the end of the batch).  The caller's buffers are DMA'd as they are: pinned memory
 // directly, pageable memory through the runtime's own staging (faster than a
 // parallel memcpy into pinned slots, profiles/r02_ab_host_path.jsonl).  The
 // bitmap comes back in one copy at the end.  Chunk sizes are multiples of 512
 // (bitmap bytes and waves stay aligned).
+static bool env_flag(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e ? e[0] == '1' : dflt;
+}
+
 static uint64_t host_chunk() {
   uint64_t c = 262144;
   if (const char* e = getenv("PBFTV_HOST_CHUNK")) c = std::max<uint64_t>(512, strtoull(e, nullptr, 10));
@@ -1046,17 +1062,20 @@ static uint64_t host_chunk() {
 }
 
 // Chunk sizes for m items: whole chunks, then a short last chunk (default
-// 65536, PBFTV_HOST_LAST), since the last chunk's verify is the one part no
+// 131072, PBFTV_HOST_LAST), since the last chunk's verify is the one part no
 // copy hides.  (Halving every chunk of the tail measured slower: each DMA
 // command costs a ~10-20 us gap on the copy engine; tools/host_path_ab.py.)
 static std::vector<uint64_t> host_chunks(uint64_t m) {
   const uint64_t c = host_chunk();
-  uint64_t last = 65536;
+  uint64_t last = 131072;  // (65536 / 32768 measured slower with the second verify stream)
   if (const char* e = getenv("PBFTV_HOST_LAST")) last = strtoull(e, nullptr, 10) / 512 * 512;
   if (last >= c || m <= c) last = 0;
+  // every chunk but the final one is a multiple of 512 (each chunk's bitmap
+  // starts on a byte): the ragged remainder joins the last chunk
+  const uint64_t head = last ? (m - last) / 512 * 512 : m;
   std::vector<uint64_t> out;
-  for (uint64_t r = m - last; r > 0; r -= std::min(c, r)) out.push_back(std::min(c, r));
-  if (last) out.push_back(last);
+  for (uint64_t r = head; r > 0; r -= std::min(c, r)) out.push_back(std::min(c, r));
+  if (m > head) out.push_back(m - head);
   return out;
 }
 
@@ -1072,6 +1091,18 @@ static int verify_host_pipelined(Device& d, const uint8_t* H, const uint8_t* S, 
   const uint64_t c = *std::max_element(chunks.begin(), chunks.end()), nch = chunks.size();
   const int ns = (int)std::min<uint64_t>(nch, host_slots());
   const size_t oh = 0, os = 32 * c, ok = 96 * c, slot = 100 * c;  // slot layout: hashes | sigs | keys
+  // every key index in one copy up front (one DMA command per chunk fewer;
+  // PBFTV_HOST_KEYS_FIRST=0 disables), and odd chunks verified on a second
+  // stream with their own scratch, so the last chunks' verifies overlap instead
+  // of queueing behind each other (PBFTV_HOST_2COMPUTE=0 disables).  Same box:
+  // pinned 2.38 -> 2.30 ms, pageable 2.46 -> 2.36 ms (profiles/r02_ab_host_path_2compute.jsonl;
+  // a second copy queue for the signatures measured no gain).
+  const bool keys_first = env_flag("PBFTV_HOST_KEYS_FIRST", true);
+  const bool two = env_flag("PBFTV_HOST_2COMPUTE", true) && nch > 1;
+  if (two) {
+    if (!d.stream2) HIP_TRY(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+    if (!d.join_ev) HIP_TRY(hipEventCreateWithFlags(&d.join_ev, hipEventDisableTiming));
+  }
   if (!d.cstream) HIP_TRY(hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking));
   for (int k = 0; k < ns; ++k) {
     if (!d.h2d_ev[k]) HIP_TRY(hipEventCreateWithFlags(&d.h2d_ev[k], hipEventDisableTiming));
@@ -1079,6 +1110,10 @@ static int verify_host_pipelined(Device& d, const uint8_t* H, const uint8_t* S, 
     HIP_TRY(d.din[k].ensure(slot + 64));
   }
   HIP_TRY(d.bitmap.ensure((m + 7) / 8 + 8));
+  if (keys_first) {
+    HIP_TRY(d.keys_all.ensure(4 * m + 64));
+    HIP_TRY(hipMemcpyAsync(d.keys_all.p, K, 4 * m, hipMemcpyHostToDevice, d.cstream));
+  }
   bool used[Device::kSlots] = {};
   uint64_t lo = 0;
   for (uint64_t j = 0; j < nch; lo += chunks[j], ++j) {
@@ -1088,14 +1123,20 @@ static int verify_host_pipelined(Device& d, const uint8_t* H, const uint8_t* S, 
     if (used[k]) HIP_TRY(hipStreamWaitEvent(d.cstream, d.comp_ev[k], 0));  // slot's previous chunk verified
     HIP_TRY(hipMemcpyAsync(dv + oh, H + 32 * lo, 32 * cnt, hipMemcpyHostToDevice, d.cstream));
     HIP_TRY(hipMemcpyAsync(dv + os, S + 64 * lo, 64 * cnt, hipMemcpyHostToDevice, d.cstream));
-    HIP_TRY(hipMemcpyAsync(dv + ok, K + lo, 4 * cnt, hipMemcpyHostToDevice, d.cstream));
+    if (!keys_first) HIP_TRY(hipMemcpyAsync(dv + ok, K + lo, 4 * cnt, hipMemcpyHostToDevice, d.cstream));
+    hipStream_t vst = two && (j & 1) ? d.stream2 : d.stream;
     HIP_TRY(hipEventRecord(d.h2d_ev[k], d.cstream));
-    HIP_TRY(hipStreamWaitEvent(d.stream, d.h2d_ev[k], 0));
-    int rc = verify_on_device(d, dv + oh, dv + os, reinterpret_cast<const uint32_t*>(dv + ok), cnt,
-                              d.bitmap.as<uint8_t>() + lo / 8, d.stream);
+    HIP_TRY(hipStreamWaitEvent(vst, d.h2d_ev[k], 0));
+    const uint32_t* kp = keys_first ? d.keys_all.as<uint32_t>() + lo : reinterpret_cast<const uint32_t*>(dv + ok);
+    int rc = verify_on_device(d, dv + oh, dv + os, kp, cnt, d.bitmap.as<uint8_t>() + lo / 8, vst,
+                              vst == d.stream2 ? &d.vs2 : nullptr);
     if (rc != PBFTV_OK) return rc;
-    HIP_TRY(hipEventRecord(d.comp_ev[k], d.stream));
+    HIP_TRY(hipEventRecord(d.comp_ev[k], vst));
     used[k] = true;
+  }
+  if (two) {  // the bitmap copy waits for both verify streams
+    HIP_TRY(hipEventRecord(d.join_ev, d.stream2));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.join_ev, 0));
   }
   HIP_TRY(hipMemcpyAsync(out_bm, d.bitmap.p, (m + 7) / 8, hipMemcpyDeviceToHost, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));

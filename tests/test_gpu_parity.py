@@ -326,12 +326,20 @@ def test_ecdsa_wave_path_edge_counts(ver, oracle_lib, monkeypatch):
 
 # ---- host-buffer pipeline (pbftv_api.cpp verify_host_pipelined) ------------
 @pytest.mark.parametrize("chunk", ["512", "4096", "262144"])
-def test_host_pipeline_chunks_pageable_and_pinned(ver, oracle_lib, chunk, monkeypatch):
-    """The chunked host-buffer path (staging copy -> DMA -> verify, two slots in
-    flight) at chunk sizes that give 1, a few and many chunks, a ragged tail,
-    from pageable numpy memory and from pbftv_host_alloc memory (no staging),
-    against the corruption mask (1 %) and the oracle on a sample."""
+@pytest.mark.parametrize("layout", ["default", "one_stream", "short_tail"])
+def test_host_pipeline_chunks_pageable_and_pinned(ver, oracle_lib, chunk, layout, monkeypatch):
+    """The chunked host-buffer path (DMA into device slots -> verify, even and
+    odd chunks on two verify streams, key indices copied up front) at chunk
+    sizes that give 1, a few and many chunks, a ragged tail, from pageable numpy
+    memory and from pbftv_host_alloc memory, against the corruption mask (1 %)
+    and the oracle on a sample.  one_stream: the round-2 layout (one verify
+    stream, keys copied per chunk); short_tail: a 1024-signature last chunk."""
     monkeypatch.setenv("PBFTV_HOST_CHUNK", chunk)
+    if layout == "one_stream":
+        monkeypatch.setenv("PBFTV_HOST_2COMPUTE", "0")
+        monkeypatch.setenv("PBFTV_HOST_KEYS_FIRST", "0")
+    if layout == "short_tail":
+        monkeypatch.setenv("PBFTV_HOST_LAST", "1024")
     keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=16, per_key=32, seed=55)
     n = 40_000 + 123
     rng = np.random.default_rng(56)

@@ -16,14 +16,16 @@ pub, H, S, K, ok = synth.config4(1 << 20, n_keys=100)
 ver = Verifier()
 ver.register_keys(pub)
 pins = [ver.pinned(a) for a in (H, S, K)]
-VARIANTS = [(262144, 0, 1), (262144, 65536, 1), (262144, 32768, 1), (262144, 0, 0), (262144, 65536, 0),
-            (131072, 32768, 0)]
+VARIANTS = [  # (full chunk, last chunk, PBFTV_HOST_KEYS_FIRST, PBFTV_HOST_2COMPUTE)
+    (262144, 65536, 0, 0), (262144, 65536, 1, 0), (262144, 65536, 1, 1), (262144, 32768, 1, 1),
+    (262144, 131072, 1, 1), (131072, 65536, 1, 1)]
 for rnd in range(2):
-    for chunk, last, stage in VARIANTS:
+    for chunk, last, kf, two in VARIANTS:
         os.environ["PBFTV_HOST_CHUNK"] = str(chunk)
         os.environ["PBFTV_HOST_LAST"] = str(last)
-        os.environ["PBFTV_HOST_STAGE"] = str(stage)
-        r = {"round": rnd, "chunk": chunk, "last": last, "stage_pageable": stage}
+        os.environ["PBFTV_HOST_KEYS_FIRST"] = str(kf)
+        os.environ["PBFTV_HOST_2COMPUTE"] = str(two)
+        r = {"round": rnd, "chunk": chunk, "last": last, "keys_first": kf, "two_compute": two}
         for label, arrays in (("pinned", tuple(p.a for p in pins)), ("pageable", (H, S, K))):
             got = ver.verify_batch(*arrays)
             ts = []
