@@ -374,16 +374,20 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
   static_assert(K >= 1 && K <= 16, "kRPowN covers R^0 .. R^17");
   const uint64_t L = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // The forward pass reads s only (32 B): an s outside (0, n) joins the
+  // products as 1.  r, the key and the hash are read once, in the backward
+  // pass, where Go's remaining checks decide the record's ok.
   fe acc, rk;
-  uint32_t okm = 0;
+  uint32_t okm = 0;  // bit j: 0 < s_j < n
   for (int j = 0; j < K; ++j) {
     const uint64_t i = lane + (uint64_t)j * L;
-    uint32_t r[8], sw[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-    bool ok = false;
+    uint32_t sw[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    bool oks = false;
     if (i < n) {
       uint32_t s[8];
-      ok = sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s);
-      if (ok) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
+      load_be256(sigs + 64 * i + 32, s);
+      oks = !words_is_zero(s) && words_lt(s, kN32);
+      if (oks) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
     }
     fe sv;
     fe_from_words(sv, sw);
@@ -391,24 +395,28 @@ __global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict
     else fn_mul(acc, acc, sv);
     if (j + 1 < K)  // c_j is read back for w_{j+1}
       PBFTV_UNROLL for (int l = 0; l < 9; ++l) prefix[((uint64_t)j * 9 + l) * L + lane] = acc.v[l];
-    okm |= (ok ? 1u : 0u) << j;
+    okm |= (oks ? 1u : 0u) << j;
   }
   fe_set(rk, kRPowN[K + 1]);
   fn_mul(acc, acc, rk);        // P R: the lane total in Montgomery form
   fe inv;
-  wave_batch_inv_n(inv, acc);  // P^-1 R: one inversion per wave (64 K signatures)
+  wave_batch_inv_n(inv, acc);  // P^-1 R: one inversion per wave (64 K signatures; one per
+                               // 256-thread block measured slower: 0.126 vs 0.120 ms)
   if (K > 1) {
     fe_set(rk, kRPowN[K]);
     fn_mul(inv, inv, rk);      // P^-1 R^K
   }
   for (int j = K - 1; j >= 0; --j) {
     const uint64_t i = lane + (uint64_t)j * L;
-    const bool ok = (okm >> j) & 1u;
+    const bool oks = (okm >> j) & 1u;
     uint32_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-    if (ok) {
-      load_be256(sigs + 64 * i, r);
-      load_be256(sigs + 64 * i + 32, s);
+    bool ok = false;
+    if (i < n) {
+      uint32_t sl[8];
+      ok = oks && sig_ok(sigs, key_idx, key_valid, nkeys, i, r, sl);  // Go's range checks + a valid key
+      if (oks) PBFTV_UNROLL for (int t = 0; t < 8; ++t) s[t] = sl[t];
     }
+    if (!ok) PBFTV_UNROLL for (int t = 0; t < 8; ++t) r[t] = 0;
     fe w;
     if (K > 1 && j > 0) {
       fe pre;
