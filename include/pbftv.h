@@ -324,9 +324,11 @@ int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uin
  * one shard per device and each shard is pipelined in chunks: DMA of the
  * caller's buffers as they are (pinned memory, e.g. from pbftv_host_alloc,
  * directly; pageable memory through the runtime's staging) on one copy
- * stream, chunks back to back into up to PBFTV_HOST_SLOTS = 16 device slots,
- * each chunk verified as it lands (PBFTV_HOST_CHUNK, default 262144
- * signatures; the last chunk PBFTV_HOST_LAST, default 65536). */
+ * stream -- every key index first, then each chunk's hashes and signatures
+ * back to back into up to PBFTV_HOST_SLOTS = 16 device slots -- and each chunk
+ * verified as it lands, even and odd chunks on two streams so the last two
+ * overlap (PBFTV_HOST_CHUNK, default 262144 signatures; the last chunk
+ * PBFTV_HOST_LAST, default 131072, takes the ragged remainder). */
 int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs,
                                   const uint32_t* key_idx, uint64_t n, uint8_t* out_bitmap);
 
