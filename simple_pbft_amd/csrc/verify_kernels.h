@@ -208,17 +208,14 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
   const uint32_t t = threadIdx.x;
   // lane p reads record p: with a key order (k_key_*) the p-th signature by key,
   // written there by stage 1 (coalesced: no gather through a permutation)
-#ifdef PBFTV_COMB_XCD
   // XCD-aware record ranges: the dispatcher deals blocks round-robin over the
-  // 8 XCDs (block b -> XCD b % 8); give XCD x the x-th eighth of the key-ordered
-  // records, so each XCD's L2 / TLB sees ~1/8 of the keys
-  const uint32_t nb = gridDim.x, b = blockIdx.x;
-  const uint32_t per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
-  const uint32_t blk = b < 8 * per ? x * per + (x < rem ? x : rem) + k : b;  // (leftover blocks keep their index)
-  const uint64_t p = (uint64_t)(rem == 0 ? blk : b) * blockDim.x + t;
-#else
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + t;
-#endif
+  // 8 XCDs (block b -> XCD b % 8), so XCD x is given the x-th eighth of the
+  // key-ordered records and its L2 and TLBs see ~1/8 of the keys (blocks past
+  // the last multiple of 8 keep their index).  Same box, 3 rounds: comb
+  // 0.9447 -> 0.9377 ms, step 1.0985 -> 1.0845 ms at 1M.
+  const uint32_t nb = gridDim.x, b = blockIdx.x, per = nb / 8;
+  const uint32_t blk = b < 8 * per ? (b % 8) * per + b / 8 : b;
+  const uint64_t p = (uint64_t)blk * blockDim.x + t;
   const SigRec* rp = rec + p;
   uint4 meta = make_uint4(0, 0, 0, 0);  // key, batch index, ok
   if (p < n) meta = rp->q[6];
