@@ -135,6 +135,29 @@ PBFTV_HD void fs_sqr(fe& r, const fe& a) {
   fs_out(r, t);
 }
 
+// r = a^2 2^-261 - b - 2 c (mod p): X3 = R^2 - PPP - 2Q with the subtraction
+// folded into the product's columns 9..16 (and its top limb) before the output
+// carry pass -- the value of fs_sqr, then the limb-wise combination and fs_norm,
+// without that combination and its separate carry pass.  b, c S-type.
+PBFTV_HD void fs_sqr_sub2(fe& r, const fe& a, const fe& b, const fe& c) {
+  PBFTV_FS_CONSTS;
+  const uint32_t cm1 = opaque_u32(0xFFFFFFFFu);  // -1 (a signed MAD subtracts a limb from a column)
+  uint64_t t[17];
+  uint32_t a2[9];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) a2[i] = a.v[i] << 1;
+  fs_cols_init(t);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    t[2 * i] += smul(a.v[i], a.v[i]);
+    PBFTV_UNROLL for (int j = i + 1; j < 9; ++j) t[i + j] += smul(a.v[i], a2[j]);
+  }
+  // - (b + 2c) 2^261: limb k lands on column 9 + k (k < 8); b_k + 2 c_k < 2^31
+  PBFTV_UNROLL for (int k = 0; k < 8; ++k) t[9 + k] += smul(b.v[k] + (c.v[k] << 1), cm1);
+  PBFTV_UNROLL for (int i = 0; i < 8; ++i) fs_digit(t, i, c8, c9, c18, c21, c24);
+  fs_digit_top(t, c9, c18, c21, c24);
+  fs_out(r, t);
+  r.v[8] = r.v[8] - b.v[8] - (c.v[8] << 1);  // limb 8 of b and c: column 17, the output's top limb
+}
+
 // r = a - b limb-wise (D-type for S-type inputs)
 PBFTV_HD void fs_sub(fe& r, const fe& a, const fe& b) {
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] - b.v[i];
@@ -187,7 +210,7 @@ struct xyzz_s {
 };
 
 PBFTV_HD void xyzz_madd_s(xyzz_s& acc, const fe& x2, const fe& y2) {
-  fe u2, s2, p, r, pp, ppp, q, r2, t, ny;
+  fe u2, s2, p, r, pp, ppp, q, t, ny;
   fs_mul(u2, x2, acc.zz);
   fs_mul(s2, y2, acc.zzz);
   fs_sub(p, u2, acc.x);                // P = U2 - X1            D
@@ -195,10 +218,8 @@ PBFTV_HD void xyzz_madd_s(xyzz_s& acc, const fe& x2, const fe& y2) {
   fs_sqr(pp, p);
   fs_mul(ppp, p, pp);
   fs_mul(q, acc.x, pp);
-  fs_sqr(r2, r);
   fe x3;
-  PBFTV_UNROLL for (int i = 0; i < 9; ++i) x3.v[i] = r2.v[i] - ppp.v[i] - (q.v[i] << 1);
-  fs_norm(x3, x3);                     // X3 = R^2 - PPP - 2Q    S
+  fs_sqr_sub2(x3, r, ppp, q);          // X3 = R^2 - PPP - 2Q    S
   fs_sub(t, q, x3);                    // Q - X3                 D
   fs_neg(ny, acc.y);                   // -Y1                    D
   fs_mul2_add(acc.y, r, t, ny, ppp);   // Y3 = R (Q - X3) - Y1 PPP, one reduction

@@ -193,6 +193,12 @@ void h_fs_mul2_add(const uint32_t* a, const uint32_t* b, const uint32_t* c, cons
   fs_mul2_add(z, x, y, u, v);
   memcpy(r, z.v, 36);
 }
+void h_fs_sqr_sub2(const uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t* r) {
+  fe x, y, u, z;
+  memcpy(x.v, a, 36); memcpy(y.v, b, 36); memcpy(u.v, c, 36);
+  fs_sqr_sub2(z, x, y, u);
+  memcpy(r, z.v, 36);
+}
 void h_fs_norm(const uint32_t* a, uint32_t* r) {
   fe x, z;
   memcpy(x.v, a, 36);

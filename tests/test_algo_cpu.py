@@ -368,7 +368,7 @@ def test_fs_mul_sqr_types_and_values(H):
         H.h_fs_mul(slimbs(la), slimbs(lb), out)
         v = check_s(out)
         assert v % P == a * b * Rinv % P
-        assert a * b / R - 1 < v < a * b / R + 1.0001 * P
+        assert a * b - R < v * R < a * b + 10001 * P * R // 10000  # exact integers (a float T / R rounds)
         H.h_fs_sqr(slimbs(lb), out)
         v = check_s(out)
         assert v % P == b * b * Rinv % P
@@ -376,6 +376,16 @@ def test_fs_mul_sqr_types_and_values(H):
         H.h_fs_mul2_add(slimbs(la), slimbs(lb), slimbs(lc), slimbs(ld), out)
         v = check_s(out)
         assert v % P == (a * b + c * d) * Rinv % P
+        # X3 = R^2 - PPP - 2Q folded into the squaring's columns (fs_sqr_sub2):
+        # the same limbs as fs_sqr, the limb-wise combination and fs_norm
+        (le, e_), (lf, f_) = rand_s(rng, ext), rand_s(rng, ext)
+        H.h_fs_sqr_sub2(slimbs(lb), slimbs(le), slimbs(lf), out)
+        got = list(out)
+        H.h_fs_sqr(slimbs(lb), out)
+        comb = [(int(out[i]) - (le[i] & 0xFFFFFFFF) - 2 * (lf[i] & 0xFFFFFFFF)) & 0xFFFFFFFF for i in range(9)]
+        H.h_fs_norm((ctypes.c_uint32 * 9)(*comb), out)
+        assert got == list(out)
+        assert sval(got) % P == (b * b * Rinv - e_ - 2 * f_) % P
         H.h_fs_canon(slimbs(lc), out)
         assert val(out) == c % P
         x = [int(y) for y in rng.integers(-(1 << 30), 1 << 30, 9)]
