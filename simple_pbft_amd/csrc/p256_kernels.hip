@@ -19,6 +19,10 @@
 namespace pbftv {
 
 // key-order sort (k_key_*): blocks of the histogram/scatter passes, largest key count sorted
+#ifndef PBFTV_SCAL_WAVES
+#define PBFTV_SCAL_WAVES 1  // min waves per SIMD for k_ecdsa_scalars (the compiler settles at 124 VGPRs: 4)
+#endif
+
 constexpr uint32_t kSortBlocks = 256;
 constexpr uint32_t kSortMaxKeys = 1024;
 constexpr uint32_t kSortHdr = kSortMaxKeys + 64;  // key-sort header: 2 x (totals | claims), words each
@@ -365,7 +369,7 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
 // for the lane fixes and the wave scans + 1/(64 K) of an inversion (round 2
 // converted every s: 6 + 14/K).
 template <int K>
-__global__ void __launch_bounds__(256) k_ecdsa_scalars(const uint8_t* __restrict__ hashes,
+__global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const uint8_t* __restrict__ hashes,
                                                        const uint8_t* __restrict__ sigs,
                                                        const uint32_t* __restrict__ key_idx, uint64_t n,
                                                        const uint32_t* __restrict__ key_valid, uint32_t nkeys,
