@@ -44,11 +44,18 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
 size_t ecdsa_record_bytes(uint64_t n);
 int scalar_batch(uint64_t n);
 size_t scalar_prefix_bytes(uint64_t n);
-// stage 1: inputs in arrival order; record of signature i written at pos[i]
-// (key order) or at i (pos == nullptr)
+// key order of a batch (stage 0 -> stage 1): per-key totals and claim
+// counters in the key-sort header; total == nullptr: arrival order
+struct KeyOrder {
+  const uint32_t* total;
+  uint32_t* claim;
+  uint32_t nkeys;
+};
+// stage 1: inputs in arrival order; record of signature i written at its
+// place in key order (placed by stage 1 itself from ko) or at i
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                                 const uint32_t* key_valid, uint32_t nkeys, void* rec, void* prefix,
-                                const uint32_t* pos, hipStream_t st);
+                                const KeyOrder& ko, hipStream_t st);
 // stage 2: (wg, wq) one of PBFTV_COMBOS; qtabs = device array of the nkeys
 // key tables' addresses (width wq each, one allocation per key).
 // okb == nullptr: records in arrival order, LSB-first bitmap (ceil(n/8) B)
@@ -57,17 +64,17 @@ hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, cons
 hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab,
                              const uint32_t* const* qtabs,
                              uint8_t* bitmap, uint8_t* okb, hipStream_t st);
-// stage 0 (optional): key order pos[i] = position of signature i sorted by key
-// (scratch: key_sort_scratch_bytes = a header of key_sort_header_bytes, which
-// must be ZERO when the scratch is first used and is left zero by every sort,
-// then pos).
+// stage 0 (optional): per-key totals for the key order (scratch:
+// key_sort_scratch_bytes = a header of key_sort_header_bytes, which must be
+// ZERO when the scratch is first used and is left zero by every batch).
+// parity: the caller's batch counter for this scratch (alternates the header's
+// two counter sets; any sequence of values that alternates is fine).  *out is
+// what stage 1 needs.
 bool key_sort_wanted(uint64_t n, uint32_t nkeys);
 size_t key_sort_header_bytes();
 size_t key_sort_scratch_bytes(uint64_t n, uint32_t nkeys);
-// parity: the caller's batch counter for this scratch (alternates the header's
-// two counter sets; any sequence of values that alternates is fine).
-hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, uint32_t parity,
-                           hipStream_t st);
+hipError_t launch_key_count(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, uint32_t parity,
+                            KeyOrder* out, hipStream_t st);
 hipError_t launch_pack_bits(const uint8_t* okb, uint64_t n, uint8_t* bitmap, hipStream_t st);
 // latency path for small batches: one wave per signature (scalars, per-window
 // points, butterfly sum, check) in one launch.  Output: okbytes[i] (one byte per

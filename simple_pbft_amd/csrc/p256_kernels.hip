@@ -341,6 +341,83 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
 }
 
 // ---------------------------------------------------------------------------
+// Key order for the comb (stage 0).  The key tables are looked up at random
+// entries; when the 64 lanes of a wave name ~50 different keys (a random
+// 100-key batch) every wave-wide table load touches ~50 tables, when they
+// share a key the lookups fall in one table window like the G lookups do.
+// Same-box A/B at 1M signatures / 100 keys (round-1 bench with the batch pre-sorted on the host): comb
+// 1.345 ms in arrival order, 1.237 ms key-sorted.  A counting sort in three
+// small launches: per-block key histograms in LDS added into per-key totals ->
+// exclusive scan of the totals -> each block claims its range of every key
+// with one atomic per (block, key) and scatters through LDS cursors.  Not
+// stable (the order inside a key does not matter: results go back to the
+// signature's own index).
+__device__ __forceinline__ void block_key_hist(uint32_t* h, const uint32_t* __restrict__ key_idx, uint64_t n,
+                                               uint32_t nkeys) {
+  const uint32_t nb = nkeys + 1;  // bin nkeys: out-of-range key indices (rejected later)
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = (uint64_t)blockIdx.x * chunk;
+  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t k = key_idx[i];
+    atomicAdd(&h[k < nkeys ? k : nkeys], 1u);
+  }
+  __syncthreads();
+}
+
+// One launch (k_key_hist: per-block histograms in LDS added into per-key
+// totals) and the scatter inside stage 1: every stage-1 block counts its own
+// signatures by key in LDS during its forward pass, scans the <= 1025 totals
+// itself (the key starts), claims its range of each key with one atomic on a
+// claim counter, and places each record through LDS cursors in its backward
+// pass.  No memset, no scan launch, no fence, no position array.  The header
+// holds two sets of per-key counters (totals, claims); batch j counts into set
+// j % 2 while k_key_hist's block 0 clears set (j + 1) % 2 for the next batch
+// (that set's last reader, batch j - 1's stage 1, finished before this launch
+// began).  Both sets start zeroed when the scratch is allocated.  Round 2
+// began with memset + hist + scan + scatter: 4 launches and two 5-us fills.
+__global__ void __launch_bounds__(256) k_key_hist(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
+                                                  uint32_t* __restrict__ cur, uint32_t* __restrict__ other) {
+  __shared__ uint32_t h[kSortMaxKeys + 1];
+  if (blockIdx.x == 0)
+    for (uint32_t b = threadIdx.x; b < 2 * kSortHdr; b += blockDim.x) other[b] = 0;
+  block_key_hist(h, key_idx, n, nkeys);
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
+    if (h[b]) atomicAdd(&cur[b], h[b]);
+}
+
+// start[b] = exclusive prefix of total[0..nkeys] (<= 1025 entries), every
+// thread of the 256-thread block; start[] is complete after the call's last
+// __syncthreads.
+__device__ __forceinline__ void block_key_starts(const uint32_t* __restrict__ total, uint32_t nkeys, uint32_t* start,
+                                                 uint32_t* part) {
+  constexpr uint32_t kPer = (kSortMaxKeys + 1 + 255) / 256;
+  const uint32_t t = threadIdx.x, m = nkeys + 1;
+  uint32_t v[kPer], sum = 0;
+  PBFTV_UNROLL for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t b = kPer * t + k;
+    v[k] = b < m ? total[b] : 0u;
+    sum += v[k];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    const uint32_t x = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  PBFTV_UNROLL for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t b = kPer * t + k;
+    if (b < m) start[b] = run;
+    run += v[k];
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
 // stage 1: scalars.  One 128-B record per signature (SigRec, verify_kernels.h):
 // u1 = e w, u2 = r w (LE words), r, the key index, the signature's batch
 // index and ok = Go's range checks passed and the key is registered and valid.
@@ -348,7 +425,8 @@ hipError_t launch_build_tables(int w, const uint32_t* keys_le, uint32_t key0, ui
 // Inputs are read in ARRIVAL order -- each lane owns K signatures i = lane +
 // j*L (j < K, L = lanes in the grid), so every input load is coalesced across
 // the wave -- and each record is written to the signature's position in key
-// order, pos[i] (k_key_scatter; identity without a key order): one full
+// order (placed through the block's LDS cursors, see block_key_starts above;
+// the batch index without a key order): one full
 // 128-B line per lane, so the comb reads its lane's record coalesced and never
 // gathers through a permutation.  The 64 K values of s of a wave share ONE
 // inversion (Montgomery's trick twice: per lane, prefix products c_j = s_0 ...
@@ -374,10 +452,18 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
                                                        const uint32_t* __restrict__ key_idx, uint64_t n,
                                                        const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                        SigRec* __restrict__ rec, uint32_t* __restrict__ prefix,
-                                                       const uint32_t* __restrict__ pos) {
+                                                       KeyOrder ko) {
   static_assert(K >= 1 && K <= 16, "kRPowN covers R^0 .. R^17");
   const uint64_t L = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // key order: this block's signatures counted per key (then its cursors)
+  __shared__ uint32_t kh[kSortMaxKeys + 1], kstart[kSortMaxKeys + 1], kpart[256];
+  const bool sorted = ko.total != nullptr;  // block-uniform
+  const uint32_t nk = ko.nkeys;
+  if (sorted) {
+    for (uint32_t b = threadIdx.x; b <= nk; b += blockDim.x) kh[b] = 0;
+    block_key_starts(ko.total, nk, kstart, kpart);  // (ends with a barrier: kh[] is clear)
+  }
   // The forward pass reads s only (32 B): an s outside (0, n) joins the
   // products as 1.  r, the key and the hash are read once, in the backward
   // pass, where Go's remaining checks decide the record's ok.
@@ -392,6 +478,10 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
       load_be256(sigs + 64 * i + 32, s);
       oks = !words_is_zero(s) && words_lt(s, kN32);
       if (oks) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
+      if (sorted) {
+        const uint32_t k = key_idx[i];
+        atomicAdd(&kh[k < nk ? k : nk], 1u);  // bin nk: out-of-range key indices (rejected below)
+      }
     }
     fe sv;
     fe_from_words(sv, sw);
@@ -403,6 +493,12 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
   }
   fe_set(rk, kRPowN[K + 1]);
   fn_mul(acc, acc, rk);        // P R: the lane total in Montgomery form
+  if (sorted) {  // claim this block's range of every key: kh[] becomes its cursors
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b <= nk; b += blockDim.x)
+      if (kh[b]) kh[b] = kstart[b] + atomicAdd(&ko.claim[b], kh[b]);
+    __syncthreads();
+  }
   fe inv;
   wave_batch_inv_n(inv, acc);  // P^-1 R: one inversion per wave (64 K signatures; one per
                                // 256-thread block measured slower: 0.126 vs 0.120 ms)
@@ -447,7 +543,12 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
         fn_canon(t, t);
         fe_to_words(u2, t);
       }
-      SigRec* o = rec + (pos != nullptr ? (uint64_t)pos[i] : i);
+      uint64_t at = i;
+      if (sorted) {
+        const uint32_t k = key_idx[i];
+        at = atomicAdd(&kh[k < nk ? k : nk], 1u);  // the signature's place in key order
+      }
+      SigRec* o = rec + at;
       o->q[0] = make_uint4(u1[0], u1[1], u1[2], u1[3]);
       o->q[1] = make_uint4(u1[4], u1[5], u1[6], u1[7]);
       o->q[2] = make_uint4(u2[0], u2[1], u2[2], u2[3]);
@@ -456,93 +557,6 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
       o->q[5] = make_uint4(r[4], r[5], r[6], r[7]);
       o->q[6] = make_uint4(ok ? key_idx[i] : 0u, (uint32_t)i, ok ? 1u : 0u, 0u);
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Key order for the comb (stage 0).  The key tables are looked up at random
-// entries; when the 64 lanes of a wave name ~50 different keys (a random
-// 100-key batch) every wave-wide table load touches ~50 tables, when they
-// share a key the lookups fall in one table window like the G lookups do.
-// Same-box A/B at 1M signatures / 100 keys (round-1 bench with the batch pre-sorted on the host): comb
-// 1.345 ms in arrival order, 1.237 ms key-sorted.  A counting sort in three
-// small launches: per-block key histograms in LDS added into per-key totals ->
-// exclusive scan of the totals -> each block claims its range of every key
-// with one atomic per (block, key) and scatters through LDS cursors.  Not
-// stable (the order inside a key does not matter: results go back to the
-// signature's own index).
-__device__ __forceinline__ void block_key_hist(uint32_t* h, const uint32_t* __restrict__ key_idx, uint64_t n,
-                                               uint32_t nkeys) {
-  const uint32_t nb = nkeys + 1;  // bin nkeys: out-of-range key indices (rejected later)
-  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
-  __syncthreads();
-  const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = (uint64_t)blockIdx.x * chunk;
-  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const uint32_t k = key_idx[i];
-    atomicAdd(&h[k < nkeys ? k : nkeys], 1u);
-  }
-  __syncthreads();
-}
-
-// Two launches, no memset, no scan launch, no fence.  The header holds two
-// sets of per-key counters (totals, claims); batch j counts into set j % 2
-// while k_key_hist's block 0 clears set (j + 1) % 2 for the next batch (that
-// set's last reader, the scatter of batch j - 1, finished before this launch
-// began).  Both sets start zeroed when the scratch is allocated.
-//   k_key_hist:    per-block histograms (LDS) added into total[];
-//   k_key_scatter: every block scans the <= 1025 totals in LDS itself (key
-//                  starts), claims its range of each key with one atomic on
-//                  claim[], and scatters through LDS cursors.
-// Round 2 had memset + hist + scan + scatter: 4 launches and two 5-us fills.
-__global__ void __launch_bounds__(256) k_key_hist(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
-                                                  uint32_t* __restrict__ cur, uint32_t* __restrict__ other) {
-  __shared__ uint32_t h[kSortMaxKeys + 1];
-  if (blockIdx.x == 0)
-    for (uint32_t b = threadIdx.x; b < 2 * kSortHdr; b += blockDim.x) other[b] = 0;
-  block_key_hist(h, key_idx, n, nkeys);
-  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
-    if (h[b]) atomicAdd(&cur[b], h[b]);
-}
-
-__global__ void __launch_bounds__(256) k_key_scatter(const uint32_t* __restrict__ key_idx, uint64_t n, uint32_t nkeys,
-                                                     const uint32_t* __restrict__ total, uint32_t* __restrict__ claim,
-                                                     uint32_t* __restrict__ pos) {
-  __shared__ uint32_t h[kSortMaxKeys + 1];
-  __shared__ uint32_t start[kSortMaxKeys + 1];
-  __shared__ uint32_t part[256];
-  // key starts: exclusive scan of total[0..nkeys], thread t owns entries kPer t ..
-  constexpr uint32_t kPer = (kSortMaxKeys + 1 + 255) / 256;
-  const uint32_t t = threadIdx.x, m = nkeys + 1;
-  uint32_t v[kPer], sum = 0;
-  PBFTV_UNROLL for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t b = kPer * t + k;
-    v[k] = b < m ? total[b] : 0u;
-    sum += v[k];
-  }
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t off = 1; off < 256; off <<= 1) {
-    const uint32_t x = t >= off ? part[t - off] : 0u;
-    __syncthreads();
-    part[t] += x;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - sum;
-  PBFTV_UNROLL for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t b = kPer * t + k;
-    if (b < m) start[b] = run;
-    run += v[k];
-  }
-  block_key_hist(h, key_idx, n, nkeys);  // (its first __syncthreads also publishes start[])
-  for (uint32_t b = threadIdx.x; b <= nkeys; b += blockDim.x)
-    if (h[b]) h[b] = start[b] + atomicAdd(&claim[b], h[b]);  // this block's range of key b
-  __syncthreads();
-  const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x, lo = (uint64_t)blockIdx.x * chunk;
-  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const uint32_t k = key_idx[i];
-    pos[i] = atomicAdd(&h[k < nkeys ? k : nkeys], 1u);  // signature i's place in key order
   }
 }
 
@@ -571,19 +585,17 @@ bool key_sort_wanted(uint64_t n, uint32_t nkeys) {
 }
 
 size_t key_sort_header_bytes() { return (size_t)(4 * kSortHdr) * 4; }
-size_t key_sort_scratch_bytes(uint64_t n, uint32_t) { return key_sort_header_bytes() + (size_t)n * 4; }
+size_t key_sort_scratch_bytes(uint64_t, uint32_t) { return key_sort_header_bytes(); }
 
-hipError_t launch_key_sort(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, uint32_t parity,
-                           hipStream_t st) {
-  if (n == 0) return hipSuccess;
+hipError_t launch_key_count(const uint32_t* key_idx, uint64_t n, uint32_t nkeys, void* scratch, uint32_t parity,
+                            KeyOrder* out, hipStream_t st) {
   if (nkeys > kSortMaxKeys) return hipErrorInvalidValue;
   uint32_t* hdr = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* cur = hdr + (parity & 1u) * 2 * kSortHdr;  // totals | claims of this batch
   uint32_t* other = hdr + (~parity & 1u) * 2 * kSortHdr;
-  uint32_t* pos = hdr + key_sort_header_bytes() / 4;
+  *out = KeyOrder{cur, cur + kSortHdr, nkeys};
+  if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_key_hist, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, cur, other);
-  hipLaunchKernelGGL(k_key_scatter, dim3(kSortBlocks), dim3(256), 0, st, key_idx, n, nkeys, cur, cur + kSortHdr,
-                     pos);
   return hipGetLastError();
 }
 
@@ -649,24 +661,24 @@ size_t scalar_prefix_bytes(uint64_t n) {
 template <int K>
 static void launch_scalars_k(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                              const uint32_t* key_valid, uint32_t nkeys, void* rec, uint32_t* prefix,
-                             const uint32_t* pos, hipStream_t st) {
+                             const KeyOrder& ko, hipStream_t st) {
   const uint64_t lanes = (n + K - 1) / K;
   const uint64_t blocks = (lanes + 255) / 256;
   hipLaunchKernelGGL(k_ecdsa_scalars<K>, dim3((uint32_t)blocks), dim3(256), 0, st, hashes, sigs, key_idx, n,
-                     key_valid, nkeys, reinterpret_cast<SigRec*>(rec), prefix, pos);
+                     key_valid, nkeys, reinterpret_cast<SigRec*>(rec), prefix, ko);
 }
 
 hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                                 const uint32_t* key_valid, uint32_t nkeys, void* rec, void* prefix,
-                                const uint32_t* pos, hipStream_t st) {
+                                const KeyOrder& ko, hipStream_t st) {
   if (n == 0) return hipSuccess;
   uint32_t* pf = reinterpret_cast<uint32_t*>(prefix);
   switch (scalar_batch(n)) {
-    case 1: launch_scalars_k<1>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
-    case 2: launch_scalars_k<2>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
-    case 4: launch_scalars_k<4>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
-    case 8: launch_scalars_k<8>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
-    default: launch_scalars_k<16>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, pos, st); break;
+    case 1: launch_scalars_k<1>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, ko, st); break;
+    case 2: launch_scalars_k<2>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, ko, st); break;
+    case 4: launch_scalars_k<4>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, ko, st); break;
+    case 8: launch_scalars_k<8>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, ko, st); break;
+    default: launch_scalars_k<16>(hashes, sigs, key_idx, n, key_valid, nkeys, rec, pf, ko, st); break;
   }
   return hipGetLastError();
 }

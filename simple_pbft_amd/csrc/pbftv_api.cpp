@@ -111,7 +111,7 @@ struct HostBuf {
 // the batched inversion, key order, per-signature result bytes).
 struct VerifyScratch {
   DevBuf rec, prefix, ksort, okb;
-  uint32_t sort_parity = 0;  // batches sorted with ksort (launch_key_sort's counter sets)
+  uint32_t sort_parity = 0;  // batches sorted with ksort (launch_key_count's counter sets)
   void release() {
     rec.release();
     prefix.release();
@@ -1020,15 +1020,15 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   HIP_TRY(sc.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
   if (!own) HIP_TRY(scratch_acquire(d, st));
   const bool sorted = pbftv::key_sort_wanted(n, d.nkeys);
+  pbftv::KeyOrder ko{nullptr, nullptr, 0};
   if (sorted) {
     HIP_TRY(sc.okb.ensure(n));  // comb lanes in key order: a wave's table lookups share keys (p256_kernels.hip k_key_*)
     HIP_TRY(ensure_key_sort(sc, n, d.nkeys, st));
-    HIP_TRY(pbftv::launch_key_sort(d_key_idx, n, d.nkeys, sc.ksort.p, sc.sort_parity++, st));
+    HIP_TRY(pbftv::launch_key_count(d_key_idx, n, d.nkeys, sc.ksort.p, sc.sort_parity++, &ko, st));
   }
-  const uint32_t* pos = sorted ? sc.ksort.as<uint32_t>() + pbftv::key_sort_header_bytes() / 4 : nullptr;
   HIP_TRY(timed(d, PBFTV_K_ECDSA_SCALARS, st, [&] {
     return pbftv::launch_ecdsa_scalars(d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(), d.nkeys, sc.rec.p,
-                                       sc.prefix.p, pos, st);
+                                       sc.prefix.p, ko, st);
   }));
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
     return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, sc.rec.p, n, d.gtab->as<uint32_t>(),
