@@ -192,6 +192,7 @@ __device__ __forceinline__ void read_entry_lds(uint4 (*sent)[PBFTV_COMB_BLOCK], 
   entry_words(e, ew);
 }
 
+
 template <int WG, int WQ>
 __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigRec* __restrict__ rec, uint64_t n,
                                                                     const uint4* __restrict__ gtab,
@@ -220,49 +221,59 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
   uint4 meta = make_uint4(0, 0, 0, 0);  // key, batch index, ok
   if (p < n) meta = rp->q[6];
   bool ok = false;
-  if (meta.z != 0) {
-    {
-      const uint4 a = rp->q[0], b = rp->q[1], c = rp->q[2], dd = rp->q[3];
-      digit_stream<WG> s1;
-      digit_stream<WQ> s2;
-      s1.w[0] = a.x; s1.w[1] = a.y; s1.w[2] = a.z; s1.w[3] = a.w;
-      s1.w[4] = b.x; s1.w[5] = b.y; s1.w[6] = b.z; s1.w[7] = b.w;
-      s2.w[0] = c.x; s2.w[1] = c.y; s2.w[2] = c.z; s2.w[3] = c.w;
-      s2.w[4] = dd.x; s2.w[5] = dd.y; s2.w[6] = dd.z; s2.w[7] = dd.w;
-      s1.carry = s2.carry = 0;
-      PBFTV_UNROLL for (int j = 0; j < S::nD; ++j)
-        sdig[j][t] = (typename S::Digit)((S::is_q(j) ? s2.next() : s1.next()) - 1);
+  // Every lane runs the step loop (no divergence around the wave-wide entry
+  // loads; comb -0.8 % same box); a lane without a valid signature has
+  // all-zero digits, reads entry 0 of the G table and adds nothing.
+  const bool act = meta.z != 0;
+  {
+    uint4 a = make_uint4(0, 0, 0, 0), b = a, c = a, dd = a;
+    if (act) {
+      a = rp->q[0];
+      b = rp->q[1];
+      c = rp->q[2];
+      dd = rp->q[3];
     }
-    const uint4* qtab = qtabs[meta.x];  // the key's own table allocation
-    xyzz_s R;  // signed-limb accumulator (fes.h)
-    bool inf = true;
-    int d = (int)sdig[0][t] + 1;
-    issue_entry_lds(sent, t, entry_ptr<WG>(gtab, 0, d));
+    digit_stream<WG> s1;
+    digit_stream<WQ> s2;
+    s1.w[0] = a.x; s1.w[1] = a.y; s1.w[2] = a.z; s1.w[3] = a.w;
+    s1.w[4] = b.x; s1.w[5] = b.y; s1.w[6] = b.z; s1.w[7] = b.w;
+    s2.w[0] = c.x; s2.w[1] = c.y; s2.w[2] = c.z; s2.w[3] = c.w;
+    s2.w[4] = dd.x; s2.w[5] = dd.y; s2.w[6] = dd.z; s2.w[7] = dd.w;
+    s1.carry = s2.carry = 0;
+    PBFTV_UNROLL for (int j = 0; j < S::nD; ++j)
+      sdig[j][t] = (typename S::Digit)((S::is_q(j) ? s2.next() : s1.next()) - 1);
+  }
+  const uint4* qtab = act ? qtabs[meta.x] : gtab;  // the key's own table allocation
+  xyzz_s R;  // signed-limb accumulator (fes.h)
+  bool inf = true;
+  int d = (int)sdig[0][t] + 1;
+  issue_entry_lds(sent, t, entry_ptr<WG>(gtab, 0, d));
 #pragma unroll 1
-    for (int j = 0; j < S::nD; ++j) {
-      uint32_t w16[16];
-      read_entry_lds(sent, t, w16);
-      const int dc = d;
-      if (j + 1 < S::nD) {  // next step's entry streams into LDS during this addition
-        d = (int)sdig[j + 1][t] + 1;
-        issue_entry_lds(sent, t, S::is_q(j + 1) ? entry_ptr<WQ>(qtab, S::win(j + 1), d)
-                                                : entry_ptr<WG>(gtab, S::win(j + 1), d));
-      }
-      if (dc != 0) {
-        fe x, y;
-        entry_to_fe(x, y, w16);
-        fs_cneg(y, y, dc < 0);  // negative digit: -y, D-type (no carry chain)
-        if (inf) {
-          R.x = x;
-          fs_norm(R.y, y);
-          fe_set(R.zz, kOneP);
-          fe_set(R.zzz, kOneP);
-          inf = false;
-        } else {
-          xyzz_madd_s(R, x, y);
-        }
+  for (int j = 0; j < S::nD; ++j) {
+    uint32_t w16[16];
+    read_entry_lds(sent, t, w16);
+    const int dc = d;
+    if (j + 1 < S::nD) {  // next step's entry streams into LDS during this addition
+      d = (int)sdig[j + 1][t] + 1;
+      issue_entry_lds(sent, t, S::is_q(j + 1) ? entry_ptr<WQ>(qtab, S::win(j + 1), d)
+                                              : entry_ptr<WG>(gtab, S::win(j + 1), d));
+    }
+    if (dc != 0) {
+      fe x, y;
+      entry_to_fe(x, y, w16);
+      fs_cneg(y, y, dc < 0);  // negative digit: -y, D-type (no carry chain)
+      if (inf) {
+        R.x = x;
+        fs_norm(R.y, y);
+        fe_set(R.zz, kOneP);
+        fe_set(R.zzz, kOneP);
+        inf = false;
+      } else {
+        xyzz_madd_s(R, x, y);
       }
     }
+  }
+  if (act) {
     if (!inf && fs_is_zero(R.zz)) {
       ok = comb2_checked_verify<WG, WQ>(rp, gtab, qtab);  // exceptional step: redo
     } else {
