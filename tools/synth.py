@@ -273,20 +273,23 @@ def config1_cluster(n_req: int = 1000, seed: int = 0x50424654) -> dict:
 
 def certs(n_keys: int, per_cert: int, n_certs: int, seed: int):
     """n_certs quorum certificates of per_cert votes over one digest each, from
-    distinct replicas of an n_keys committee (configs 2 and 3)."""
+    distinct replicas of an n_keys committee (configs 2 and 3, and the QC
+    latency's one-certificate calls): every signature distinct."""
     s = Signer(n_keys, seed)
     rng = np.random.default_rng(seed)
-    H = np.zeros((n_certs * per_cert, 32), np.uint8)
-    S = np.zeros((n_certs * per_cert, 64), np.uint8)
-    K = np.zeros(n_certs * per_cert, np.uint32)
-    for c in range(n_certs):
-        h = rng.bytes(32)
-        signers = rng.choice(n_keys, per_cert, replace=False)
-        for j, k in enumerate(signers):
-            i = c * per_cert + j
-            H[i] = np.frombuffer(h, np.uint8)
-            S[i] = np.frombuffer(s.sign(h, int(k)), np.uint8)
-            K[i] = k
+    m = n_certs * per_cert
+    H = np.repeat(np.frombuffer(rng.bytes(32 * n_certs), np.uint8).reshape(n_certs, 32), per_cert, axis=0)
+    K = np.concatenate([rng.choice(n_keys, per_cert, replace=False) for _ in range(n_certs)]).astype(np.uint32)
+    S = np.zeros((m, 64), np.uint8)
+    B = _batch_signer() if m >= 4096 else None
+    if B is not None:
+        rc = B.synth_sign_batch(s.priv.ctypes.data, n_keys, H.ctypes.data, K.ctypes.data, m, S.ctypes.data,
+                                max(1, min(16, os.cpu_count() or 1)))
+        if rc != 0:
+            raise RuntimeError(f"synth_sign_batch failed: {rc}")
+    else:
+        for i in range(m):
+            S[i] = np.frombuffer(s.sign(H[i].tobytes(), int(K[i])), np.uint8)
     pub = s.pub.copy()
     s.close()
     return pub, H, S, K
