@@ -91,10 +91,8 @@ def test_config4_full_size_host_path(ver, cfg4):
 
 
 def test_config3_full_size_quorum(ver):
-    per, n_certs, pool = 67, 10000, 500
-    pub, H, S, K = synth.certs(100, per, pool, seed=per * 7 + 100)
-    reps = n_certs // pool
-    H, S, K = np.tile(H, (reps, 1)), np.tile(S, (reps, 1)), np.tile(K, reps)
+    per, n_certs = 67, 10000
+    pub, H, S, K = synth.certs(100, per, n_certs, seed=per * 7 + 100)  # 670k distinct signatures
     rng = np.random.default_rng(3)
     bad_certs = rng.choice(n_certs, n_certs // 100, replace=False)
     bad_sig = bad_certs * per + rng.integers(0, per, len(bad_certs))
