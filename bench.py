@@ -82,6 +82,14 @@ def macs_comb(gbits: int, qbits: int) -> float:
 INV_N_MACS = 25 * (36 + 54) + 162
 
 
+GATHER_ONLY_TBPS = 1.2  # 21 random 64-B gathers per lane over 1M lanes, no arithmetic (gather_calib)
+
+
+def table_points(gb: int, qb: int) -> int:
+    """Table points per verify: windows of the G and the key geometry (one 64-B entry each)."""
+    return len(window_widths(gb)) + len(window_widths(qb))
+
+
 def macs_scalars(k: int) -> float:
     """k signatures per lane, 64 k per wave share one inversion (Montgomery's trick per
     lane and across the wave over PLAIN s values, p256_kernels.hip k_ecdsa_scalars /
@@ -589,6 +597,16 @@ def main():
                            "valu_busy_frac": pmc.get("valu_busy_frac"),
                            "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
                            "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc else None}
+        if dom == "ecdsa_comb":
+            # the comb's other bound: random 64-B table gathers (one entry per table point,
+            # ~21 per verify); tools/gather_calib.hip moves the same bytes in the same shape
+            # with no arithmetic at ~1.2 TB/s (profiles/r02_gather_calib.txt)
+            pts = table_points(gb, qb)
+            gbytes = n * pts * 64
+            out["roofline"]["table_gathers"] = {"bytes_per_launch": gbytes, "points_per_verify": pts,
+                                                "TBps": gbytes / max(comb_avg, 1e-12) / 1e12,
+                                                "gather_only_TBps": GATHER_ONLY_TBPS,
+                                                "source": "tools/gather_calib.hip, profiles/r02_gather_calib.txt"}
         out["kernels"] = kern
         out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
         out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "what": "pbftv_register_keys: G table + the key tables built on the device (incl. allocation)"}

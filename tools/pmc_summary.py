@@ -11,8 +11,12 @@ derived figures the roofline claims rest on:
                      / (1024 SIMDs x cycles), with the issue costs measured by
                      tools/mad_issue_bench.hip at 4 waves/SIMD (c64: v_mad_u64_u32 /
                      v_mad_i64_i32 / 64-bit shifts and adds; c32: 32-bit VALU)
-  hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB; FETCH doubled for
-                     gfx950 wide reads, MI355X_MICROARCH.md HBM/rocprofv3 section)
+  hbm_bytes_per_launch = f x FETCH_SIZE + WRITE_SIZE (KiB; f = 2 for coalesced
+                     wide reads, MI355X_MICROARCH.md HBM/rocprofv3 section; f = 1
+                     for the comb, whose traffic is random 64-B table gathers,
+                     which FETCH_SIZE counts at their size: tools/gather_calib.hip
+                     measured 1.12x the gathered bytes for 64-B gathers and 0.50x
+                     for 128-B ones, profiles/r02_gather_calib.txt)
   kernel_ms        = mean dispatch duration in the (profiled) kernel trace
 
     python tools/pmc_summary.py gpurun_out/pmc [issue-cost file] > profiles/rNN_pmc.json
@@ -102,13 +106,16 @@ def main(d: str, costs: str | None):
                 if c in m:
                     e[c + "_frac"] = m[c] / m["SQ_WAVE_CYCLES"]
         if "FETCH_SIZE" in m or "WRITE_SIZE" in m:
-            e["hbm_bytes_per_launch"] = 2 * 1024 * m.get("FETCH_SIZE", 0) + 1024 * m.get("WRITE_SIZE", 0)
+            f = 1 if k == "ecdsa_comb" else 2  # 64-B random gathers: counted at size (gather_calib)
+            e["hbm_bytes_per_launch"] = f * 1024 * m.get("FETCH_SIZE", 0) + 1024 * m.get("WRITE_SIZE", 0)
+            e["fetch_factor"] = f
         if k == "ecdsa_comb" and len(geom) == 1:
             e["geometry"] = list(next(iter(geom)))  # bench.py uses these figures only for this geometry
         out[k] = e
     res = {"source": "rocprofv3 --pmc, separate passes (tools/pmc_passes.sh) over tools/pmc_workload.py "
                      "(config-4 verify, config-5 digests, one n=4 certificate); means over dispatches; "
-                     "FETCH_SIZE/WRITE_SIZE in KiB, FETCH doubled (gfx950); GRBM_GUI_ACTIVE / 8 XCDs",
+                     "FETCH_SIZE/WRITE_SIZE in KiB, FETCH doubled (gfx950 wide reads) except for the comb's "
+                     "64-B gathers (fetch_factor 1, tools/gather_calib.hip); GRBM_GUI_ACTIVE / 8 XCDs",
            "issue_costs": {"c64": c64, "c32": c32, "from": costs or "defaults"},
            "kernels": out}
     json.dump(res, sys.stdout, indent=1)
