@@ -15,23 +15,27 @@
 
 constexpr int kSteps = 21;
 
-template <int S>
+// M independent entries in flight per lane per step (memory-level parallelism)
+template <int S, int M = 1>
 __device__ __forceinline__ void gather(const uint4* __restrict__ tab, uint64_t entries, uint32_t seed,
                                        uint32_t* __restrict__ sink) {
-  __shared__ uint4 buf[S / 16][256];
+  __shared__ uint4 buf[M * S / 16][256];
   const uint32_t t = threadIdx.x, wb = t & ~63u;
   uint64_t x = (uint64_t)(blockIdx.x * 256u + t) * 0x9E3779B97F4A7C15ull + seed;
   uint32_t acc = 0;
-  for (int s = 0; s < kSteps; ++s) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdull;
-    x ^= x >> 29;
-    const uint4* p = tab + (x % entries) * (S / 16);
+  for (int s = 0; s < kSteps; s += M) {
 #pragma unroll
-    for (int k = 0; k < S / 16; ++k) __builtin_amdgcn_global_load_lds(p + k, &buf[k][wb], 16, 0, 0);
+    for (int m = 0; m < M; ++m) {
+      x ^= x >> 33;
+      x *= 0xff51afd7ed558ccdull;
+      x ^= x >> 29;
+      const uint4* p = tab + (x % entries) * (S / 16);
+#pragma unroll
+      for (int k = 0; k < S / 16; ++k) __builtin_amdgcn_global_load_lds(p + k, &buf[m * (S / 16) + k][wb], 16, 0, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int k = 0; k < S / 16; ++k) acc += buf[k][t].x;
+    for (int k = 0; k < M * S / 16; ++k) acc += buf[k][t].x;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   if (acc == 0x12345678u) sink[0] = acc;  // keeps the loads
@@ -42,6 +46,9 @@ __global__ void __launch_bounds__(256) k_gather64(const uint4* tab, uint64_t ent
 }
 __global__ void __launch_bounds__(256) k_gather128(const uint4* tab, uint64_t entries, uint32_t seed, uint32_t* sink) {
   gather<128>(tab, entries, seed, sink);
+}
+__global__ void __launch_bounds__(256) k_gather64x3(const uint4* tab, uint64_t entries, uint32_t seed, uint32_t* sink) {
+  gather<64, 3>(tab, entries, seed, sink);
 }
 
 int main() {
@@ -69,10 +76,17 @@ int main() {
     hipEventRecord(b);
     hipEventSynchronize(b);
     hipEventElapsedTime(&ms128, a, b);
+    float ms64x3 = 0;
+    hipEventRecord(a);
+    hipLaunchKernelGGL(k_gather64x3, dim3(blocks), dim3(256), 0, 0, tab, bytes / 64, 53u + rep, sink);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(&ms64x3, a, b);
     const double g64 = (double)lanes * kSteps * 64, g128 = (double)lanes * kSteps * 128;
     printf("{\"rep\": %d, \"gather64\": {\"bytes\": %.0f, \"ms\": %.4f, \"GBps\": %.1f}, "
-           "\"gather128\": {\"bytes\": %.0f, \"ms\": %.4f, \"GBps\": %.1f}}\n",
-           rep, g64, ms64, g64 / ms64 / 1e6, g128, ms128, g128 / ms128 / 1e6);
+           "\"gather128\": {\"bytes\": %.0f, \"ms\": %.4f, \"GBps\": %.1f}, "
+           "\"gather64_3_in_flight\": {\"bytes\": %.0f, \"ms\": %.4f, \"GBps\": %.1f}}\n",
+           rep, g64, ms64, g64 / ms64 / 1e6, g128, ms128, g128 / ms128 / 1e6, g64, ms64x3, g64 / ms64x3 / 1e6);
   }
   hipFree(tab);
   hipFree(sink);
