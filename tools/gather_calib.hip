@@ -16,7 +16,7 @@
 constexpr int kSteps = 21;
 
 // M independent entries in flight per lane per step (memory-level parallelism)
-template <int S, int M = 1>
+template <int S, int M = 1, int AUX = 0>
 __device__ __forceinline__ void gather(const uint4* __restrict__ tab, uint64_t entries, uint32_t seed,
                                        uint32_t* __restrict__ sink) {
   __shared__ uint4 buf[M * S / 16][256];
@@ -31,7 +31,7 @@ __device__ __forceinline__ void gather(const uint4* __restrict__ tab, uint64_t e
       x ^= x >> 29;
       const uint4* p = tab + (x % entries) * (S / 16);
 #pragma unroll
-      for (int k = 0; k < S / 16; ++k) __builtin_amdgcn_global_load_lds(p + k, &buf[m * (S / 16) + k][wb], 16, 0, 0);
+      for (int k = 0; k < S / 16; ++k) __builtin_amdgcn_global_load_lds(p + k, &buf[m * (S / 16) + k][wb], 16, 0, AUX);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -49,6 +49,12 @@ __global__ void __launch_bounds__(256) k_gather128(const uint4* tab, uint64_t en
 }
 __global__ void __launch_bounds__(256) k_gather64x3(const uint4* tab, uint64_t entries, uint32_t seed, uint32_t* sink) {
   gather<64, 3>(tab, entries, seed, sink);
+}
+__global__ void __launch_bounds__(256) k_gather64nt(const uint4* tab, uint64_t entries, uint32_t seed, uint32_t* sink) {
+  gather<64, 1, 2>(tab, entries, seed, sink);  // nt (aux = 2)
+}
+__global__ void __launch_bounds__(256) k_gather64sc(const uint4* tab, uint64_t entries, uint32_t seed, uint32_t* sink) {
+  gather<64, 1, 3>(tab, entries, seed, sink);  // sc0 | nt
 }
 
 int main() {
@@ -82,6 +88,18 @@ int main() {
     hipEventRecord(b);
     hipEventSynchronize(b);
     hipEventElapsedTime(&ms64x3, a, b);
+    float msnt = 0, mssc = 0;
+    hipEventRecord(a);
+    hipLaunchKernelGGL(k_gather64nt, dim3(blocks), dim3(256), 0, 0, tab, bytes / 64, 71u + rep, sink);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(&msnt, a, b);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(k_gather64sc, dim3(blocks), dim3(256), 0, 0, tab, bytes / 64, 73u + rep, sink);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(&mssc, a, b);
+    printf("{\"rep\": %d, \"gather64_nt\": {\"ms\": %.4f}, \"gather64_aux3\": {\"ms\": %.4f}}\n", rep, msnt, mssc);
     const double g64 = (double)lanes * kSteps * 64, g128 = (double)lanes * kSteps * 128;
     printf("{\"rep\": %d, \"gather64\": {\"bytes\": %.0f, \"ms\": %.4f, \"GBps\": %.1f}, "
            "\"gather128\": {\"bytes\": %.0f, \"ms\": %.4f, \"GBps\": %.1f}, "
