@@ -566,7 +566,7 @@ def main():
         "warmup": args.warmup, "warmup_steps_run": w, "ms_per_step": t_max / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": mode, "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic (OpenSSL-signed P-256 votes, tools/synth.py)",
+        "data": "synthetic: distinct OpenSSL-signed P-256 votes, 1% corrupted (tools/synth.py)",
         "config": {"workload": (f"config4: {n_global} ECDSA-P256 sigs" +
                                 (f" ({args.n} per rank)" if args.weak else f" sharded N/{ws}") +
                                 f", {args.keys}-key table, 1% corrupted (8 classes)"),
