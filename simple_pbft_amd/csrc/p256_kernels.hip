@@ -458,6 +458,11 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
   const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // key order: this block's signatures counted per key (then its cursors)
   __shared__ uint32_t kh[kSortMaxKeys + 1], kstart[kSortMaxKeys + 1], kpart[256];
+  // the lane's prefix products c_0 .. c_{K-2}: in LDS for K <= 4 (27.6 KB per
+  // block at K = 4, no HBM round trip: 57 MB per launch at 1M), else in the
+  // global scratch (each thread reads back only what it wrote)
+  constexpr bool kPrefixLds = K <= 4;
+  __shared__ uint32_t spre[kPrefixLds ? (K > 1 ? K - 1 : 1) : 1][9][256];
   const bool sorted = ko.total != nullptr;  // block-uniform
   const uint32_t nk = ko.nkeys;
   if (sorted) {
@@ -487,8 +492,13 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
     fe_from_words(sv, sw);
     if (j == 0) acc = sv;
     else fn_mul(acc, acc, sv);
-    if (j + 1 < K)  // c_j is read back for w_{j+1}
-      PBFTV_UNROLL for (int l = 0; l < 9; ++l) prefix[((uint64_t)j * 9 + l) * L + lane] = acc.v[l];
+    if (j + 1 < K) {  // c_j is read back for w_{j+1}
+      if constexpr (kPrefixLds) {
+        PBFTV_UNROLL for (int l = 0; l < 9; ++l) spre[j][l][threadIdx.x] = acc.v[l];
+      } else {
+        PBFTV_UNROLL for (int l = 0; l < 9; ++l) prefix[((uint64_t)j * 9 + l) * L + lane] = acc.v[l];
+      }
+    }
     okm |= (oks ? 1u : 0u) << j;
   }
   fe_set(rk, kRPowN[K + 1]);
@@ -520,7 +530,11 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
     fe w;
     if (K > 1 && j > 0) {
       fe pre;
-      PBFTV_UNROLL for (int l = 0; l < 9; ++l) pre.v[l] = prefix[((uint64_t)(j - 1) * 9 + l) * L + lane];
+      if constexpr (kPrefixLds) {
+        PBFTV_UNROLL for (int l = 0; l < 9; ++l) pre.v[l] = spre[j - 1][l][threadIdx.x];
+      } else {
+        PBFTV_UNROLL for (int l = 0; l < 9; ++l) pre.v[l] = prefix[((uint64_t)(j - 1) * 9 + l) * L + lane];
+      }
       fn_mul(w, inv, pre);     // s_j^-1 R
       fe sv;
       fe_from_words(sv, s);
