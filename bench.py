@@ -199,7 +199,52 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def _cpu_verify(so_name, fn_name, pub, H, S, K, sample: int):
+def _read(path: str):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def cpu_allotment() -> dict:
+    """The host CPUs this process may actually use, with the evidence: the
+    scheduler affinity mask (os.sched_getaffinity), the cgroup-v2 CPU quota
+    (/sys/fs/cgroup/cpu.max, "max" = none; cgroup v1 cfs_quota/period as a
+    fallback), and the physical cores / SMT threads behind the allowed CPUs
+    (/sys/devices/system/cpu/cpuN/topology).  `threads` = min(affinity,
+    floor(quota)) is what the CPU baselines run on."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    quota = None
+    cm = _read("/sys/fs/cgroup/cpu.max")
+    src = "/sys/fs/cgroup/cpu.max"
+    if cm:
+        q, _, per = cm.partition(" ")
+        if q != "max" and per:
+            quota = int(q) / int(per)
+    else:
+        q, per = _read("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"), _read("/sys/fs/cgroup/cpu/cpu.cfs_period_us")
+        src = "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+        if q and per and int(q) > 0:
+            quota = int(q) / int(per)
+    cores = set()
+    for c in aff:
+        pkg = _read(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id")
+        core = _read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id")
+        if core is not None:
+            cores.add((pkg, core))
+    threads = len(aff)
+    if quota is not None:
+        threads = max(1, min(threads, int(quota)))
+    return {"threads": threads, "affinity_cpus": len(aff), "cgroup_quota_cpus": quota,
+            "cgroup_cpu_max": cm, "cgroup_source": src if cm is not None or quota is not None else None,
+            "physical_cores_in_affinity": len(cores) or None,
+            "smt_threads_per_core": (len(aff) / len(cores)) if cores else None,
+            "smt_active": _read("/sys/devices/system/cpu/smt/active"), "nproc": os.cpu_count(),
+            "cpu_model": cpu_model()}
+
+
+def _cpu_verify(so_name, fn_name, pub, H, S, K, sample: int, threads: int):
     so = os.path.join(ROOT, "oracle", so_name)
     if not os.path.exists(so):
         return None
@@ -207,23 +252,22 @@ def _cpu_verify(so_name, fn_name, pub, H, S, K, sample: int):
     vp = ctypes.c_void_p
     fn = getattr(L, fn_name)
     fn.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_int]
-    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 cores
     h, s, k = (np.ascontiguousarray(a[:sample]) for a in (H, S, K))
     bm = np.zeros((sample + 7) // 8, np.uint8)
     t0 = time.perf_counter()
     fn(h.ctypes.data, s.ctypes.data, k.ctypes.data, sample, pub.ctypes.data, len(pub), bm.ctypes.data, threads)
     dt = time.perf_counter() - t0
     return {"value": sample / dt, "unit": "verifies/s", "cores": threads, "nproc": os.cpu_count(),
-            "cpu_model": cpu_model(), "_bitmap": bm}
+            "cpu_model": cpu_model(), "seconds": dt, "_bitmap": bm}
 
 
-def openssl_standin(pub, H, S, K, sample: int):
+def openssl_standin(pub, H, S, K, sample: int, threads: int):
     """cpu_baseline: OpenSSL 3 libcrypto ECDSA_do_verify on host threads
     (oracle/openssl_standin.c).  Go 1.19's amd64 P-256
     (crypto/elliptic p256_asm) is a port of OpenSSL's nistz256 assembly, so this
     is the faithful stand-in for the reference's CPU verify path, which cannot
     run here (no Go toolchain)."""
-    r = _cpu_verify("libopenssl_standin.so", "standin_ecdsa_p256_verify_batch", pub, H, S, K, sample)
+    r = _cpu_verify("libopenssl_standin.so", "standin_ecdsa_p256_verify_batch", pub, H, S, K, sample, threads)
     if r is not None:
         r["kind"] = "openssl_standin"
         r["sample"] = (f"first {sample} signatures of the config-4 batch (oracle/openssl_standin.c, {r['cores']} "
@@ -231,11 +275,19 @@ def openssl_standin(pub, H, S, K, sample: int):
     return r
 
 
-def cpu_oracle_port(pub, H, S, K, sample: int):
+def cpu_standin_sample(threads: int, n: int) -> int:
+    """A bounded sample: ~0.5 s of wall time at ~27k verifies/s per thread,
+    at least 262,144 signatures (~10 thread-seconds), at most the batch, in
+    whole 512-signature groups."""
+    want = max(262144, threads * 27_000 // 2)
+    return n if want >= n else want // 512 * 512
+
+
+def cpu_oracle_port(pub, H, S, K, sample: int, threads: int):
     """The oracle port (oracle/p256_ref.c: 4x64-bit CIOS, bit-serial Shamir --
     deliberately simple, for parity) on host threads; reported beside the
     stand-in, not as the baseline."""
-    r = _cpu_verify("liboracle.so", "oracle_ecdsa_p256_verify_batch", pub, H, S, K, sample)
+    r = _cpu_verify("liboracle.so", "oracle_ecdsa_p256_verify_batch", pub, H, S, K, sample, threads)
     if r is not None:
         r["kind"] = "port"
         r["sample"] = f"first {sample} signatures of the config-4 batch (oracle/p256_ref.c, {r['cores']} pthreads)"
@@ -282,7 +334,7 @@ def _timed(ver, fn, reps):
     return min(ts), float(np.median(ts))
 
 
-def run_config1(ver, n_req=1000):
+def run_config1(ver, n_req=1000, outputs=None):
     """configs[0]: the reference 4-node pattern for 1k requests with every
     message signed, end to end from host buffers, one device
     round trip per message kind (Go-JSON preimage + SHA-256 + checks + ECDSA on
@@ -295,8 +347,13 @@ def run_config1(ver, n_req=1000):
       votes        pbftv_flush_votes: 9 prepare + 12 commit receipts/request,
                    verifyMsg against the request's State + signature
       replies      pbftv_flush_replies: 4 per request, the client checks them
-    The messages are laid out column-wise before timing, as a cgo shim would
-    hand over a pool snapshot."""
+    2 % of each message kind is corrupted (synth.config1_cluster: bad
+    signatures; validly signed pre-prepares/votes with a wrong digest, wrong
+    view or stale sequence ID), and every bit of every flush is compared with
+    the construction (check_config1).  The messages are laid out column-wise
+    before timing, as a cgo shim would hand over a pool snapshot.  `outputs`
+    (a dict) receives the inputs and the last flush results (for the GPU test's
+    oracle comparison)."""
     from simple_pbft_amd.pbftv import PrePrepareColumns, ReplyColumns, RequestColumns, VoteColumns
     c = synth.config1_cluster(n_req)
     ver.register_keys(c["pub"])
@@ -307,22 +364,23 @@ def run_config1(ver, n_req=1000):
         return np.array([x[1] for x in checks if x[0] == kind], np.int64)
     qi, pi, vi, ri = idx("request"), idx("preprepare"), idx("vote"), idx("reply")
     votes, replies, pps = c["votes"], c["replies"], c["preprepares"]
-    seq_to_r = {int(s): r for r, s in enumerate(c["assigned_seqs"])}
     req_cols = RequestColumns([c["requests"][j] for j in qi])
     qS, qK = np.ascontiguousarray(c["request_sigs"][qi]), np.full(len(qi), synth.CLIENT_KEY, np.uint32)
     aseq = np.ascontiguousarray(c["assigned_seqs"][qi])
     pp_cols = PrePrepareColumns([pps[j] for j in pi])          # one entry per replica receipt
     pS, pK = np.ascontiguousarray(c["preprepare_sigs"][pi]), np.zeros(len(pi), np.uint32)
-    p_state = np.array([seq_to_r[pps[j][1]] for j in pi], np.uint32)
+    p_state = np.ascontiguousarray(c["preprepare_state"][pi])
     vote_cols = VoteColumns([votes[j] for j in vi])            # one entry per received vote
     vS = np.ascontiguousarray(c["vote_sigs"][vi])
     vK = np.array([node_of[votes[j][3]] for j in vi], np.uint32)
-    v_state = np.array([seq_to_r[votes[j][1]] for j in vi], np.uint32)
-    s_view = np.full(n_req, synth.VIEW, np.int64)
-    s_last = np.full(n_req, -1, np.int64)
+    v_state = np.ascontiguousarray(c["vote_state"][vi])
+    s_view, s_last = c["state_view"], c["state_last"]
     rep_cols = ReplyColumns([replies[j] for j in ri])
     rS = np.ascontiguousarray(c["reply_sigs"][ri])
     rK = np.array([node_of[replies[j][3]] for j in ri], np.uint32)
+    expect = {"request_sig": c["request_sig_ok"][qi], "preprepare_sig": c["preprepare_sig_ok"][pi],
+              "preprepare_msg": c["preprepare_msg_ok"][pi], "vote_sig": c["vote_sig_ok"][vi],
+              "vote_msg": c["vote_msg_ok"][vi], "reply_sig": c["reply_sig_ok"][ri]}
     state = {}
 
     def flow():
@@ -330,31 +388,78 @@ def run_config1(ver, n_req=1000):
         _, _, p_ok, pm_ok = ver.flush_preprepares(pp_cols, pS, pK, (s_view, s_last), p_state, digests=False)
         _, v_ok, vm_ok = ver.flush_votes(vote_cols, vS, vK, (s_view, s_last, req_d), v_state, digests=False)
         _, r_ok = ver.flush_replies(rep_cols, rS, rK, digests=False)
-        state["ok"] = bool(q_ok.all() and p_ok.all() and pm_ok.all() and v_ok.all() and vm_ok.all() and r_ok.all())
+        state["got"] = {"request_sig": q_ok, "preprepare_sig": p_ok, "preprepare_msg": pm_ok, "vote_sig": v_ok,
+                        "vote_msg": vm_ok, "reply_sig": r_ok, "request_digests": req_d}
 
     best, med = _timed(ver, flow, 5)
     n_sig = len(qi) + len(pi) + len(vi) + len(ri)
     n_dig = 2 * len(qi) + 2 * len(pi) + len(vi) + len(ri)
+    ok, rejected = check_config1(state["got"], expect)
+    if outputs is not None:
+        outputs.update(cluster=c, got=state["got"], expect=expect, index={"request": qi, "preprepare": pi,
+                                                                          "vote": vi, "reply": ri})
     return {"workload": f"config1: 4-node pattern, {n_req} requests, every message signed: {n_sig} signature "
                         f"checks ({len(qi)} requests, {len(pi)} pre-prepares, {len(vi)} votes, {len(ri)} replies), "
                         f"{n_dig} Go-JSON digests built on the device, {len(pi) + len(vi)} verifyMsg, "
-                        "4 flush calls end-to-end from host buffers",
-            "verifies_per_s": n_sig / best, "ms": best * 1e3, "ms_median": med * 1e3, "check": state.get("ok")}
+                        "4 flush calls end-to-end from host buffers; 2% of each message kind corrupted",
+            "verifies_per_s": n_sig / best, "ms": best * 1e3, "ms_median": med * 1e3, "rejected": rejected,
+            "check": ok}
 
 
-def run_certs(ver, n_keys, per_cert, n_certs, label):
+def check_config1(got: dict, expect: dict):
+    """Every bit of every config-1 flush equals the construction, and each flush
+    rejects >= 1 % of its receipts, some for a bad signature (so an all-accept
+    verifier fails).  Returns
+    (ok, rejected receipts per output)."""
+    ok = True
+    rejected = {}
+    for k, want in expect.items():
+        g = np.asarray(got[k], bool)
+        ok = ok and g.shape == want.shape and bool((g == want).all())
+        rejected[k] = int((~want).sum())
+    for kind in ("request", "preprepare", "vote", "reply"):
+        bad = ~expect[kind + "_sig"]
+        if kind + "_msg" in expect:
+            bad = bad | ~expect[kind + "_msg"]
+        ok = ok and bad.sum() >= 0.01 * len(bad) and (kind + "_sig") in rejected and rejected[kind + "_sig"] > 0
+    return bool(ok), rejected
+
+
+def run_certs(ver, n_keys, per_cert, n_certs, label, outputs=None):
+    """Configs 2 and 3: n_certs quorum certificates of per_cert distinct votes in
+    ONE device-resident launch; 1 % of the certificates carry one bad vote and
+    0.5 % two (synth.corrupt_certs, the 8 corruption classes in turn).  The
+    check: every bit equals the construction, the 2f+1 QC fails exactly at the
+    certificates with a bad vote, and the reference's 2f count
+    (pbft_impl.go:212,227) exactly at those with two."""
     pub, H, S, K = synth.certs(n_keys, per_cert, n_certs, seed=per_cert * 7 + n_keys)  # every signature distinct
+    want, bad_any, bad_two = synth.corrupt_certs(H, S, K, per_cert, n_keys)
     ver.register_keys(pub)
     n = len(K)
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
     db = ver.alloc(0, (n + 7) // 8)
     best, med = _timed(ver, lambda: ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr), 10)
-    bits = np.unpackbits(db.to_host(), bitorder="little")[:n].reshape(n_certs, per_cert)
-    quorum_ok = bool((bits.sum(1) >= per_cert).all())
+    bits = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
     for b in (dh, ds, dk, db):
         b.free()
-    return {"workload": label, "verifies_per_s": n / best, "ms": best * 1e3, "ms_median": med * 1e3,
-            "certs": n_certs, "check": quorum_ok}
+    f = (per_cert - 1) // 2
+    ok = check_certs(bits, want, per_cert, bad_any, bad_two, quorum_ref=2 * f)
+    if outputs is not None:
+        outputs.update(pub=pub, H=H, S=S, K=K, bits=bits, want=want, bad_any=bad_any, bad_two=bad_two)
+    return {"workload": label + "; 1% of certificates with one bad vote, 0.5% with two", "verifies_per_s": n / best,
+            "ms": best * 1e3, "ms_median": med * 1e3, "certs": n_certs, "rejected": int((~want).sum()), "check": ok}
+
+
+def check_certs(bits, want, per_cert, bad_any, bad_two, quorum_ref):
+    """Bits equal the construction; QC (all per_cert votes, 2f+1 of n = 3f+1)
+    fails exactly at bad_any; the reference's >= 2f count exactly at bad_two."""
+    bits = np.asarray(bits, bool)
+    n_certs = len(bits) // per_cert
+    acc = bits.reshape(n_certs, per_cert).sum(1)
+    qc_fail = np.nonzero(acc < per_cert)[0]
+    ref_fail = np.nonzero(acc < quorum_ref)[0]
+    return bool(len(bad_any) > 0 and (bits == want).all() and np.array_equal(qc_fail, np.sort(bad_any))
+                and np.array_equal(ref_fail, np.sort(bad_two)))
 
 
 def run_config5(ver, n=1_000_000, steps=5):
@@ -388,24 +493,41 @@ def _sha_run(ver, data, off, ln, steps, label):
     dord, dg = ver.alloc(0, 4 * n), ver.alloc(0, 32 * n)
     ver.sha256_order_dev(0, dl.ptr, n, dord.ptr)
     ver.sync(0)
+    # wall clock and kernel time over exactly the same calls: one untimed
+    # warm-up call, then per rep the HIP-event kernel time (library events on
+    # the launch stream) and the wall time around the same synchronised call;
+    # the kernel runs inside its wall window, so kernel_ms <= ms rep by rep
+    ver.sha256_batch_dev(0, dd.ptr, do.ptr, dl.ptr, dord.ptr, n, dg.ptr)
+    ver.sync(0)
     ver.set_kernel_timing(True)
-    ver.reset_kernel_times()
-    best, med = _timed(ver, lambda: ver.sha256_batch_dev(0, dd.ptr, do.ptr, dl.ptr, dord.ptr, n, dg.ptr), steps)
-    k_ms, k_cnt = ver.kernel_time_ms(0, 2)
+    walls, kerns = [], []
+    for _ in range(steps):
+        ver.reset_kernel_times()
+        t0 = time.perf_counter()
+        ver.sha256_batch_dev(0, dd.ptr, do.ptr, dl.ptr, dord.ptr, n, dg.ptr)
+        ver.sync(0)
+        walls.append(time.perf_counter() - t0)
+        k_ms, k_cnt = ver.kernel_time_ms(0, 2)
+        assert k_cnt == 1
+        kerns.append(k_ms * 1e-3)
     ver.set_kernel_timing(False)
+    wall, kavg = float(np.mean(walls)), float(np.mean(kerns))
+    best = wall
     dig = dg.to_host().reshape(n, 32)
     rng = np.random.default_rng(1)
     ok = all(dig[i].tobytes() == hashlib.sha256(data[off[i]:off[i] + ln[i]].tobytes()).digest()
              for i in rng.integers(0, n, 2000))
     total = int(ln.sum())
     blocks = int(((ln.astype(np.int64) + 8) // 64 + 1).sum())
-    kavg = k_ms / max(k_cnt, 1) * 1e-3
     for b in (dd, do, dl, dord, dg):
         b.free()
     ops = blocks * SHA_OPS_PER_BLOCK
     cpu = openssl_sha256(data, off, ln, dig)
     return {"workload": label.format(n=n, lens=lo_hi(ln), gb=total / 1e9, blocks=blocks), "cpu_baseline": cpu,
             "digests_per_s": n / best, "GB_per_s": total / best / 1e9, "ms": best * 1e3, "kernel_ms": kavg * 1e3,
+            "ms_min": min(walls) * 1e3, "kernel_ms_per_rep": [k * 1e3 for k in kerns], "reps": steps,
+            "timing": "ms = mean wall time of `reps` synchronised calls; kernel_ms = mean HIP-event time of k_sha256 "
+                      "in the same calls (frac from kernel_ms)",
             "roofline": {"bound": "valu", "achieved": ops / kavg / 1e12, "peak": VALU_PEAK / 1e12,
                          "unit": "T VALU ops/s (1528 per 64-B block, SURVEY §8(d))",
                          "frac": ops / kavg / VALU_PEAK, "hbm_GB_per_s": (total + 32 * n) / kavg / 1e9,
@@ -426,7 +548,7 @@ def openssl_sha256(data, off, ln, gpu_digests):
     n = len(ln)
     off64, ln32 = np.ascontiguousarray(off, np.uint64), np.ascontiguousarray(ln, np.uint32)
     out = np.zeros((n, 32), np.uint8)
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_allotment()["threads"]
     ts = []
     for _ in range(3):
         t0 = time.perf_counter()
@@ -435,7 +557,8 @@ def openssl_sha256(data, off, ln, gpu_digests):
     t = min(ts)
     return {"value": n / t, "unit": "digests/s", "GB_per_s": float(ln32.sum()) / t / 1e9, "cores": threads,
             "nproc": os.cpu_count(), "cpu_model": cpu_model(), "kind": "openssl_standin",
-            "sample": f"all {n} messages (oracle/openssl_standin.c EVP_Digest, {threads} pthreads)",
+            "sample": f"all {n} messages (oracle/openssl_standin.c EVP_Digest, {threads} pthreads = the process's "
+                      "CPU allotment)",
             "agrees_with_gpu": bool((out == gpu_digests).all())}
 
 
@@ -619,15 +742,27 @@ def main():
                                     "p99_n100_67sigs": p99_100, "calls": {"n4": 10000, "n100": 2000},
                                     "definition": "host submit -> accept bitmap + quorum on host, pbftv_qc_verify, "
                                                   "one certificate per call (SURVEY.md §8(d))"}
-            sample = 262144
-            cb = openssl_standin(pub, H, S, K, sample=sample)
+            # the CPU baseline on every host CPU this process may use (affinity
+            # mask capped by the cgroup quota, with the evidence), plus the
+            # 16-thread figure of the box's nominal per-GPU share as a labelled extra
+            allot = cpu_allotment()
+            thr = allot["threads"]
+            sample = cpu_standin_sample(thr, n)
+            cb = openssl_standin(pub, H, S, K, sample=sample, threads=thr)
             if cb is not None:
                 bm = cb.pop("_bitmap")
                 cb["agrees_with_gpu"] = bool((np.unpackbits(bm, bitorder="little")[:sample].astype(bool) ==
                                               got[:sample]).all())
+                cb["allotment"] = allot
                 out["cpu_baseline"] = cb
                 out["gpu_vs_cpu"] = value / cb["value"]
-            port = cpu_oracle_port(pub, H, S, K, sample=32768)
+                if thr != 16:
+                    s16 = cpu_standin_sample(16, n)
+                    c16 = openssl_standin(pub, H, S, K, sample=s16, threads=min(16, thr))
+                    if c16 is not None:
+                        c16.pop("_bitmap")
+                        out["cpu_baseline_16_threads"] = c16
+            port = cpu_oracle_port(pub, H, S, K, sample=32768, threads=min(thr, 64))
             if port is not None:
                 bm = port.pop("_bitmap")
                 port["agrees_with_gpu"] = bool((np.unpackbits(bm, bitorder="little")[:32768].astype(bool) ==

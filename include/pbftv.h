@@ -301,7 +301,13 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
  * table): pbftv_add_keys appends k keys as indices nkeys .. nkeys + k - 1 at the
  * registered geometry (PBFTV_ENOMEM if their tables do not fit);
  * pbftv_set_key replaces key `index` (< nkeys) in place.  Both need a prior
- * pbftv_register_keys and wait for the device's queued work first. */
+ * pbftv_register_keys.  They, and pbftv_register_keys, first wait for ALL work
+ * queued on the GPU (hipDeviceSynchronize: verifies enqueued on caller
+ * streams by the *_dev entry points included), so no verify in flight reads a
+ * table, validity flag or table pointer while it is rewritten.  If any device
+ * fails, every device of the context drops its key set (PBFTV_ENOKEYS until
+ * the next successful pbftv_register_keys), so shards never disagree on the
+ * keys. */
 int pbftv_add_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid);
 int pbftv_set_key(pbftv_ctx* ctx, uint32_t index, const uint8_t* pub_xy, uint8_t* out_valid);
 

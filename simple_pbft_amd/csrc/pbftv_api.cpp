@@ -251,8 +251,15 @@ hipError_t collect_times(Device& d) {
 
 // G comb tables by (HIP device, width): built once and shared by every
 // context (and aliased logical device) on that GPU while one holds it.
+// g_tables_mu guards the map only; a table is built under its own slot's
+// build mutex, so GPUs build their G tables in parallel and lookups of other
+// widths or devices never wait for a build.
+struct GSlot {
+  std::weak_ptr<DevBuf> tab;
+  std::shared_ptr<std::mutex> build = std::make_shared<std::mutex>();
+};
 std::mutex g_tables_mu;
-std::map<std::pair<int, int>, std::weak_ptr<DevBuf>> g_tables;
+std::map<std::pair<int, int>, GSlot> g_tables;
 
 struct pbftv_ctx {
   std::vector<std::unique_ptr<Device>> devs;
@@ -906,7 +913,10 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     HIP_TRY(hipSetDevice(d.id));
     auto t0 = std::chrono::steady_clock::now();
     d.have_keys = false;
-    HIP_TRY(hipStreamSynchronize(d.stream));
+    // every stream of the GPU, not only ours: a verify enqueued on a caller
+    // stream (pbftv_stream_create + *_dev) may still read the tables, key_valid
+    // or qptrs this call rewrites in place
+    HIP_TRY(hipDeviceSynchronize());
     size_t free_b = 0, total_b = 0, held = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     for (auto& b : d.qblocks) held += b->cap;  // the old key tables' HBM counts for the new ones
@@ -915,7 +925,7 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     choose_bits(k, free_b + held, &wg, &wq, [&](int g) {
       std::lock_guard<std::mutex> gl(g_tables_mu);
       auto it = g_tables.find({dev_id, g});
-      return it != g_tables.end() && !it->second.expired();  // ours or another context's: no new HBM
+      return it != g_tables.end() && !it->second.tab.expired();  // ours or another context's: no new HBM
     });
     d.nkeys = 0;
     if (wq != d.qbits || d.qtab.size() < k) {  // new width or too few slots: new blocks (freeing HBM
@@ -927,9 +937,16 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     if (d.gbits != wg || !d.gtab) {  // G table: once per GPU and width while any context holds it
       d.gtab.reset();
       d.gbits = 0;
-      std::lock_guard<std::mutex> gl(g_tables_mu);
-      auto& slot = g_tables[{d.id, wg}];
-      d.gtab = slot.lock();
+      std::shared_ptr<std::mutex> build_mu;
+      {
+        std::lock_guard<std::mutex> gl(g_tables_mu);
+        build_mu = g_tables[{d.id, wg}].build;
+      }
+      std::lock_guard<std::mutex> bl(*build_mu);  // one builder per (GPU, width); others wait here, not globally
+      {
+        std::lock_guard<std::mutex> gl(g_tables_mu);
+        d.gtab = g_tables[{d.id, wg}].tab.lock();
+      }
       if (!d.gtab) {
         auto t = std::make_shared<DevBuf>();
         HIP_TRY(t->ensure(pbftv::table_bytes(wg)));
@@ -939,7 +956,10 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
         const int r = build_tables(d, wg, nullptr, 0, 1, 1, dummy.as<uint32_t>(), {t->p});
         if (r != PBFTV_OK) return r;
         trace("G table build", d.id, t0);
-        slot = t;
+        {
+          std::lock_guard<std::mutex> gl(g_tables_mu);
+          g_tables[{d.id, wg}].tab = t;
+        }
         d.gtab = std::move(t);
       }
       d.gbits = wg;
@@ -950,7 +970,13 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     d.have_keys = true;
     return PBFTV_OK;
   });
-  if (rc != PBFTV_OK) return rc;
+  if (rc != PBFTV_OK) {
+    for (auto& dp : ctx->devs) {  // no device keeps a key set the others lack
+      std::lock_guard<std::mutex> lk(dp->mu);
+      dp->have_keys = false;
+    }
+    return rc;
+  }
   if (out_valid)
     for (uint32_t j = 0; j < k; ++j) out_valid[j] = valid[j] ? 1 : 0;
   return PBFTV_OK;
@@ -964,10 +990,18 @@ int pbftv_add_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* o
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    HIP_TRY(hipStreamSynchronize(d.stream));
+    HIP_TRY(hipDeviceSynchronize());  // caller streams too: qptrs and key_valid are rewritten
     return build_key_tables(d, le, d.nkeys, k, first ? valid.data() : nullptr);
   });
-  if (rc != PBFTV_OK) return rc;
+  if (rc != PBFTV_OK) {
+    // a device that failed (or succeeded) leaves the key counts disagreeing
+    // across shards: every device is unusable until the caller re-registers
+    for (auto& dp : ctx->devs) {
+      std::lock_guard<std::mutex> lk(dp->mu);
+      dp->have_keys = false;
+    }
+    return rc;
+  }
   if (out_valid)
     for (uint32_t j = 0; j < k; ++j) out_valid[j] = valid[j] ? 1 : 0;
   return PBFTV_OK;
@@ -983,10 +1017,16 @@ int pbftv_set_key(pbftv_ctx* ctx, uint32_t index, const uint8_t* pub_xy, uint8_t
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    HIP_TRY(hipStreamSynchronize(d.stream));  // no verify still reads the old table
+    HIP_TRY(hipDeviceSynchronize());  // no verify on any stream (caller streams too) still reads the old table
     return build_key_tables(d, le, index, 1, first ? &valid : nullptr);
   });
-  if (rc != PBFTV_OK) return rc;
+  if (rc != PBFTV_OK) {
+    for (auto& dp : ctx->devs) {  // devices may now disagree on key `index`: re-register first
+      std::lock_guard<std::mutex> lk(dp->mu);
+      dp->have_keys = false;
+    }
+    return rc;
+  }
   if (out_valid) *out_valid = valid ? 1 : 0;
   return PBFTV_OK;
 }

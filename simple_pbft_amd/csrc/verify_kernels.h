@@ -918,13 +918,18 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
     return;
   }
   // one bit of the LSB-first bitmap: set or clear it with a word atomic
-  // (other signatures' waves share the byte; no pre-zeroing needed)
+  // (other signatures' waves share the byte; no pre-zeroing needed).  The last
+  // signature also clears the padding bits above it in its byte, so the tail
+  // of the bitmap is deterministic (as the lane path's ballot bytes are).
   uint8_t* byte = bitmap + (i >> 3);
   const uintptr_t a = reinterpret_cast<uintptr_t>(byte);
   unsigned int* word = reinterpret_cast<unsigned int*>(a & ~(uintptr_t)3);
-  const unsigned int bit = 1u << (((unsigned)(a & 3) << 3) + (unsigned)(i & 7));
+  const unsigned int sh = (unsigned)(a & 3) << 3;
+  const unsigned int bit = 1u << (sh + (unsigned)(i & 7));
+  unsigned int clear = ok ? 0u : bit;
+  if (i + 1 == n) clear |= ((0xFEu << (unsigned)(i & 7)) & 0xFFu) << sh;
+  if (clear) atomicAnd(word, ~clear);
   if (ok) atomicOr(word, bit);
-  else atomicAnd(word, ~bit);
 }
 
 template <int WG, int WQ>

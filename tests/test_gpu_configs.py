@@ -8,8 +8,12 @@ round 2 they were checked only inside bench.py):
   config 3  10,000 certificates of 67 signatures (n = 100, 2f + 1 = 67), 1 % of
             the certificates carrying one bad vote: the quorum must fail
             exactly there;
-  config 1  the 4-node, 1000-request pattern with every message signed,
-            through the four flushes (bench.run_config1's flow and check).
+  config 2  20,000 certificates of 3 signatures (n = 4) in one launch, 1 % with
+            one bad vote and 0.5 % with two: QC and the reference's 2f count
+            must fail exactly there;
+  config 1  the 4-node, 1000-request pattern with every message signed and
+            2 % of each kind corrupted, through the four flushes
+            (bench.run_config1's flow and check), against the oracle.
 
 Signatures come from OpenSSL (tools/synth.py), an implementation independent of
 both the product and the oracle.
@@ -106,8 +110,57 @@ def test_config3_full_size_quorum(ver):
     assert not quorum[bad_certs].any() and quorum.sum() == n_certs - len(bad_certs)
 
 
-def test_config1_every_message_signed(ver):
+def test_config2_full_size_quorum(ver, oracle_lib):
+    """configs[1] at its workload: n = 4 keys, 10k requests x (prepare QC +
+    commit QC) = 20,000 certificates x 3 distinct signatures = 60,000 in ONE
+    verify_batch_dev launch (<= 8 keys: the lane path without the key sort).
+    1 % of the certificates carry one bad vote, 0.5 % two, over the 8 classes
+    (synth.corrupt_certs).  Every bit equals the construction; the 2f+1 = 3 QC
+    fails exactly where a vote is bad and the reference's 2f = 2 count
+    (pbft_impl.go:212,227) exactly where two are; the oracle agrees on every
+    corrupted index and a sample."""
     import bench
-    r = bench.run_config1(ver)
+    out = {}
+    r = bench.run_certs(ver, 4, 3, 20000, "config2", outputs=out)
+    assert r["check"], r
+    assert len(out["K"]) == 60000 and r["rejected"] == 200 + 2 * 100
+    want, bits = out["want"], out["bits"]
+    sample = np.union1d(np.nonzero(~want)[0], np.arange(0, 60000, 13))
+    h, s, k = (np.ascontiguousarray(out[x][sample]) for x in ("H", "S", "K"))
+    bm = np.zeros((len(sample) + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(h.ctypes.data, s.ctypes.data, k.ctypes.data, len(sample),
+                                              out["pub"].ctypes.data, 4, bm.ctypes.data, 16)
+    assert (np.unpackbits(bm, bitorder="little")[:len(sample)].astype(bool) == bits[sample]).all()
+    # the same certificates one at a time through pbftv_qc_verify (the latency path)
+    for c in list(out["bad_two"][:3]) + list(np.setdiff1d(out["bad_any"], out["bad_two"])[:3]) + [0, 1, 2]:
+        sl = slice(3 * int(c), 3 * int(c) + 3)
+        got, acc, ok3 = ver.qc_verify(out["H"][sl], out["S"][sl], out["K"][sl], quorum=3)
+        assert (got == want[sl]).all() and acc == int(want[sl].sum())
+        assert ok3 == (c not in out["bad_any"])
+        _, _, ok2 = ver.qc_verify(out["H"][sl], out["S"][sl], out["K"][sl], quorum=2)
+        assert ok2 == (c not in out["bad_two"])
+
+
+def test_config1_every_message_signed(ver, oracle_lib):
+    """configs[0] through the four flushes with 2 % of each message kind
+    corrupted (bad signatures; validly signed pre-prepares/votes with a wrong
+    digest, wrong view or stale sequence ID): every bit equals the
+    construction (bench.check_config1) and the oracle -- oracle/gojson.py
+    preimages + the oracle verify + oracle_verify_msg against each receipt's
+    State -- and the StartConsensus digests equal the oracle's."""
+    import bench
+    import hashlib
+    from test_synth import _config1_oracle
+    out = {}
+    r = bench.run_config1(ver, outputs=out)
     assert r["check"], r
     assert "29000 signature checks" in r["workload"]
+    c, got, idx = out["cluster"], out["got"], out["index"]
+    want = _config1_oracle(oracle_lib, c)
+    for k in ("request_sig", "preprepare_sig", "preprepare_msg", "vote_sig", "vote_msg", "reply_sig"):
+        kind = k.split("_")[0]
+        assert (np.asarray(got[k]) == want[k][idx[kind]]).all(), k
+    from oracle import gojson
+    req_d = [hashlib.sha256(gojson.request(q[0], q[1], q[2], int(a))).digest()
+             for q, a in zip(c["requests"], c["assigned_seqs"])]
+    assert [bytes(x) for x in got["request_digests"]] == [req_d[j] for j in idx["request"]]

@@ -127,3 +127,79 @@ def test_two_device_registration_geometry(two_devices, oracle_lib):
     assert v.add_keys(keys[:1]).all()          # both logical devices get the new table
     K2 = np.concatenate([K, np.full(4, 3, np.uint32)])
     assert v.verify_batch(np.concatenate([H, H[:4]]), np.concatenate([S, S[:4]]), K2).all()
+
+
+@pytest.mark.parametrize("path_n", [64, 40_000])  # the wave kernel (<= 2048) and the lane path
+def test_set_key_waits_for_caller_stream_verifies(oracle_lib, path_n, monkeypatch):
+    """a verify enqueued on a CALLER stream (pbftv_stream_create +
+    verify_batch_dev) must still see the old key table when pbftv_set_key
+    replaces that key right after the enqueue: set_key waits for every stream
+    of the GPU before it rewrites the table in place."""
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_GBITS", "24")
+    monkeypatch.setenv("PBFTV_QBITS", "16")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, 4, 16, seed=73)
+    rng = np.random.default_rng(74)
+    o = rng.integers(0, len(kidx), path_n)
+    H, S, K = hashes[o].copy(), sigs[o].copy(), kidx[o].copy()
+    with Verifier(device_mask=1) as v:
+        assert v.register_keys(keys).all()
+        bufs = [v.to_device(0, H), v.to_device(0, S), v.to_device(0, K), v.alloc(0, (path_n + 7) // 8)]
+        side = v.stream_create(0)
+        try:
+            for _ in range(3):
+                bufs[3].zero()
+                v.verify_batch_dev(0, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, path_n, bufs[3].ptr, stream=side)
+                assert v.set_key(0, keys[1])  # key 0 now holds key 1's point
+                v.stream_wait(0, side)
+                got = np.unpackbits(bufs[3].to_host(), bitorder="little")[:path_n].astype(bool)
+                assert got.all(), "a verify queued before set_key saw the new table"
+                assert v.set_key(0, keys[0])
+            # after the change, key-0 signatures fail under index 0
+            v.set_key(0, keys[1])
+            got = v.verify_batch(H, S, K)
+            assert got.tolist() == (K != 0).tolist()
+        finally:
+            v.stream_destroy(0, side)
+            for b in bufs:
+                b.free()
+
+
+def test_bitmap_padding_bits_are_zero(oracle_lib, monkeypatch):
+    """bits past n in the last bitmap byte are 0 on every path, even
+    when the buffer held ones before: the wave kernel on a device buffer, and
+    the host pipeline whose chunks take the wave kernel (PBFTV_HOST_CHUNK=512,
+    a ragged last chunk after a batch that set those bits)."""
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_GBITS", "24")
+    monkeypatch.setenv("PBFTV_QBITS", "16")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, 3, 8, seed=75)
+    with Verifier(device_mask=1) as v:
+        assert v.register_keys(keys).all()
+        for n in (1, 5, 13, 24):
+            dh, ds, dk = v.to_device(0, hashes[:n]), v.to_device(0, sigs[:n]), v.to_device(0, kidx[:n])
+            db = v.alloc(0, 4)
+            v._L.pbftv_memset_dev(v._h, 0, db.ptr, 0xFF, 4)
+            v.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
+            v.sync(0)
+            raw = db.to_host()
+            bits = np.unpackbits(raw, bitorder="little")
+            nb = (n + 7) // 8
+            assert bits[:n].all() and not bits[n:8 * nb].any(), (n, raw)
+            assert (raw[nb:] == 0xFF).all()  # bytes past the bitmap untouched
+            for b in (dh, ds, dk, db):
+                b.free()
+        monkeypatch.setenv("PBFTV_HOST_CHUNK", "512")
+        # n > 2048: the call takes the pipeline, whose 512-signature chunks take the wave kernel
+        reps = 3000 // len(kidx) + 1
+        H, S, K = np.tile(hashes, (reps, 1)), np.tile(sigs, (reps, 1)), np.tile(kidx, reps)
+        assert v.verify_batch(H[:3000], S[:3000], K[:3000]).all()
+        L = v._L
+        for n in (2999, 2993):
+            bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+            rc = L.pbftv_ecdsa_p256_verify_batch(v._h, np.ascontiguousarray(H[:n]).ctypes.data,
+                                                 np.ascontiguousarray(S[:n]).ctypes.data,
+                                                 np.ascontiguousarray(K[:n]).ctypes.data, n, bm.ctypes.data)
+            assert rc == 0
+            bits = np.unpackbits(bm[:(n + 7) // 8], bitorder="little")
+            assert bits[:n].all() and not bits[n:].any(), n

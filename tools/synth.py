@@ -140,31 +140,35 @@ def signed_pool(n_keys: int, pool: int, seed: int):
     return pub, hashes, sigs, kidx
 
 
+def corrupt_one(hashes, sigs, kidx, i: int, c: int, n_keys: int, rng):
+    """Apply corruption class c (CLASSES[c]) to signature i in place."""
+    nb = N_ORDER.to_bytes(32, "big")
+    if c == 0:
+        sigs[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+    elif c == 1:
+        sigs[i, 32 + rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+    elif c == 2:
+        hashes[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
+    elif c == 3:
+        kidx[i] = (kidx[i] + 1 + rng.integers(0, n_keys - 1)) % n_keys
+    elif c == 4:
+        sigs[i, :32] = 0
+    elif c == 5:
+        sigs[i, 32:] = 0
+    elif c == 6:
+        sigs[i, :32] = np.frombuffer(nb, np.uint8)
+    else:
+        sigs[i, 32:] = 0xFF
+
+
 def corrupt(hashes, sigs, kidx, n_keys: int, frac: float, seed: int):
     """Corrupt a seeded `frac` subset in place, evenly over CLASSES; returns the expected accept mask."""
     n = len(kidx)
     rng = np.random.default_rng(seed ^ 0x5A5A)
     m = int(round(n * frac))
     idx = rng.choice(n, m, replace=False)
-    nb = N_ORDER.to_bytes(32, "big")
     for t, i in enumerate(idx):
-        c = t % 8
-        if c == 0:
-            sigs[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
-        elif c == 1:
-            sigs[i, 32 + rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
-        elif c == 2:
-            hashes[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))
-        elif c == 3:
-            kidx[i] = (kidx[i] + 1 + rng.integers(0, n_keys - 1)) % n_keys
-        elif c == 4:
-            sigs[i, :32] = 0
-        elif c == 5:
-            sigs[i, 32:] = 0
-        elif c == 6:
-            sigs[i, :32] = np.frombuffer(nb, np.uint8)
-        else:
-            sigs[i, 32:] = 0xFF
+        corrupt_one(hashes, sigs, kidx, int(i), t % 8, n_keys, rng)
     ok = np.ones(n, bool)
     ok[idx] = False
     return ok
@@ -215,8 +219,13 @@ VIEW = 10000000000                                                         # nod
 
 CLIENT_KEY = 4  # key index of the (one) client process in config 1
 
+# corruption classes of the config-1 flushes (a Byzantine sender's messages):
+# a bad signature, or a validly signed message that State.verifyMsg rejects
+# (pbft_impl.go:176-202) -- wrong digest, wrong view, stale sequence ID
+MSG_CLASSES = ["bad signature", "wrong digest", "wrong view", "stale sequence"]
 
-def config1_cluster(n_req: int = 1000, seed: int = 0x50424654) -> dict:
+
+def config1_cluster(n_req: int = 1000, seed: int = 0x50424654, bad_frac: float = 0.02) -> dict:
     """the reference's 4-node message pattern for n_req
     requests, every message signed.  Per request: the client's
     request verified by the primary (1), the primary's pre-prepare verified by
@@ -225,50 +234,130 @@ def config1_cluster(n_req: int = 1000, seed: int = 0x50424654) -> dict:
     signature checks over 13 distinct signed messages.  Keys: the 4 nodes
     (NODES order) and the client (CLIENT_KEY).  The client signs its request
     with sequenceID 0 (as sent); StartConsensus assigns the sequence ID
-    (pbft_impl.go:57-67) before the request digest is taken."""
+    (pbft_impl.go:57-67) before the request digest is taken.
+
+    Request i's consensus State has ViewID = VIEW and LastSequenceID = the
+    previous request's sequence ID (-1 for the first): the state created after
+    request i-1 committed.  A seeded `bad_frac` of each message kind (requests
+    and replies: bad signature; pre-prepares and votes: MSG_CLASSES in turn,
+    from request 1 on so that a stale sequence exists) is corrupted; the
+    expected outcome of every message is returned with it ("*_sig_ok",
+    "*_msg_ok"), so an all-accept verifier fails the check."""
     sys_path_fix()
     from simple_pbft_amd import pbftv as gj  # host-only Go-JSON encoder of the product (no GPU)
     s = Signer(5, seed)
-    sent, assigned, req_sig = [], [], []
-    pps, pp_sig = [], []
-    votes, vote_sig, replies, reply_sig = [], [], [], []
+    rng = np.random.default_rng(seed ^ 0xC0FF)
+    n_votes_per = 7
+    bad_req = set(rng.choice(n_req, int(round(n_req * bad_frac)), replace=False).tolist())
+    elig = n_req - 1
+    bad_pp = rng.choice(elig, max(4, int(round(n_req * bad_frac))), replace=False) + 1
+    bad_pp = {int(i): t % 4 for t, i in enumerate(bad_pp)}
+    nv = n_req * n_votes_per
+    bad_v = rng.choice(nv - n_votes_per, max(4, int(round(nv * bad_frac))), replace=False) + n_votes_per
+    bad_v = {int(i): t % 4 for t, i in enumerate(bad_v)}
+    bad_rep = set(rng.choice(4 * n_req, int(round(4 * n_req * bad_frac)), replace=False).tolist())
+    sent, assigned, req_sig, req_ok = [], [], [], []
+    pps, pp_sig, pp_state, pp_sig_ok, pp_msg_ok = [], [], [], [], []
+    votes, vote_sig, vote_state, vote_sig_ok, vote_msg_ok = [], [], [], [], []
+    replies, reply_sig, reply_ok = [], [], []
     checks = []  # (kind, index, receiver)
+
+    def flip(sig):
+        b = bytearray(sig)
+        b[int(rng.integers(0, 64))] ^= 1 << int(rng.integers(0, 8))
+        return bytes(b)
+
+    def tamper(view, seq, d, cls, i):
+        """(view, seq, digest) of a corrupted message of class cls for request i."""
+        if cls == 1:
+            d = hashlib.sha256(b"other request %d" % i).hexdigest().encode()
+        elif cls == 2:
+            view += 1
+        elif cls == 3:
+            seq = assigned[i - 1]  # == the state's LastSequenceID: already committed
+        return view, seq, d
+
     for i in range(n_req):
         req0 = (1668519246 + i, b"client%d" % i, b"printf", 0)
         sent.append(req0)
-        req_sig.append(s.sign(hashlib.sha256(gj.gojson_request(*req0)).digest(), CLIENT_KEY))
+        sg = s.sign(hashlib.sha256(gj.gojson_request(*req0)).digest(), CLIENT_KEY)
+        req_sig.append(flip(sg) if i in bad_req else sg)
+        req_ok.append(i not in bad_req)
         seq = 1668519247222762700 + 1000 * i
         assigned.append(seq)
         req = req0[:3] + (seq,)
         checks.append(("request", i, 0))
         d = hashlib.sha256(gj.gojson_request(*req)).hexdigest().encode()
-        pp = (VIEW, seq, d, req)
+        cls = bad_pp.get(i, -1)
+        view_p, seq_p, d_p = tamper(VIEW, seq, d, cls, i) if cls > 0 else (VIEW, seq, d)
+        pp = (view_p, seq_p, d_p, req)
         pps.append(pp)
-        pp_sig.append(s.sign(hashlib.sha256(gj.gojson_preprepare(*pp)).digest(), 0))
+        sg = s.sign(hashlib.sha256(gj.gojson_preprepare(*pp)).digest(), 0)
+        pp_sig.append(flip(sg) if cls == 0 else sg)
+        pp_state.append(i)
+        pp_sig_ok.append(cls != 0)
+        pp_msg_ok.append(cls <= 0)
         checks += [("preprepare", len(pps) - 1, r) for r in (1, 2, 3)]
-        for sender in (1, 2, 3):                       # prepares from the replicas
-            v = (VIEW, seq, d, NODES[sender], 0)
+        senders = [(x, 0) for x in (1, 2, 3)] + [(x, 1) for x in range(4)]  # prepares, then commits
+        for sender, mtype in senders:
+            j = len(votes)
+            cls = bad_v.get(j, -1)
+            view_v, seq_v, d_v = tamper(VIEW, seq, d, cls, i) if cls > 0 else (VIEW, seq, d)
+            v = (view_v, seq_v, d_v, NODES[sender], mtype)
             votes.append(v)
-            vote_sig.append(s.sign(hashlib.sha256(gj.gojson_vote(*v)).digest(), sender))
-            checks += [("vote", len(votes) - 1, r) for r in range(4) if r != sender]
-        for sender in range(4):                        # commits from every node
-            v = (VIEW, seq, d, NODES[sender], 1)
-            votes.append(v)
-            vote_sig.append(s.sign(hashlib.sha256(gj.gojson_vote(*v)).digest(), sender))
-            checks += [("vote", len(votes) - 1, r) for r in range(4) if r != sender]
+            sg = s.sign(hashlib.sha256(gj.gojson_vote(*v)).digest(), sender)
+            vote_sig.append(flip(sg) if cls == 0 else sg)
+            vote_state.append(i)
+            vote_sig_ok.append(cls != 0)
+            vote_msg_ok.append(cls <= 0)
+            checks += [("vote", j, r) for r in range(4) if r != sender]
         for sender in range(4):                        # replies to the client
+            j = len(replies)
             rp = (VIEW, req[0], req[1], NODES[sender], b"Executed")
             replies.append(rp)
-            reply_sig.append(s.sign(hashlib.sha256(gj.gojson_reply(*rp)).digest(), sender))
-            checks.append(("reply", len(replies) - 1, 4))
+            sg = s.sign(hashlib.sha256(gj.gojson_reply(*rp)).digest(), sender)
+            reply_sig.append(flip(sg) if j in bad_rep else sg)
+            reply_ok.append(j not in bad_rep)
+            checks.append(("reply", j, 4))
     pub = s.pub.copy()
     s.close()
 
     def rows(sigs):
         return np.frombuffer(b"".join(sigs), np.uint8).reshape(-1, 64)
+    s_last = np.array([-1] + assigned[:-1], np.int64)
     return {"pub": pub, "requests": sent, "request_sigs": rows(req_sig), "assigned_seqs": np.array(assigned, np.int64),
             "preprepares": pps, "preprepare_sigs": rows(pp_sig), "votes": votes, "vote_sigs": rows(vote_sig),
-            "replies": replies, "reply_sigs": rows(reply_sig), "checks": checks}
+            "replies": replies, "reply_sigs": rows(reply_sig), "checks": checks,
+            "state_view": np.full(n_req, VIEW, np.int64), "state_last": s_last,
+            "preprepare_state": np.array(pp_state, np.uint32), "vote_state": np.array(vote_state, np.uint32),
+            "request_sig_ok": np.array(req_ok), "preprepare_sig_ok": np.array(pp_sig_ok),
+            "preprepare_msg_ok": np.array(pp_msg_ok), "vote_sig_ok": np.array(vote_sig_ok),
+            "vote_msg_ok": np.array(vote_msg_ok), "reply_sig_ok": np.array(reply_ok),
+            "preprepare_class": bad_pp, "vote_class": bad_v}
+
+
+def corrupt_certs(H, S, K, per_cert: int, n_keys: int, frac_one: float = 0.01, frac_two: float = 0.005,
+                  seed: int = 0x50424654):
+    """Configs 2/3 with Byzantine votes: a seeded `frac_one` of the certificates
+    carry one bad vote and `frac_two` carry two, the votes corrupted over
+    CLASSES in turn (in place).  Returns (expected accept mask, certificates
+    with >= 1 bad vote, certificates with >= 2).  With n = 3f + 1 a QC of 2f + 1
+    votes fails at one bad vote; the reference's 2f count
+    (pbft_impl.go:212,227) fails only at two."""
+    n_certs = len(K) // per_cert
+    rng = np.random.default_rng(seed ^ 0xCE27)
+    m1, m2 = int(round(n_certs * frac_one)), int(round(n_certs * frac_two))
+    chosen = rng.choice(n_certs, m1 + m2, replace=False)
+    one, two = np.sort(chosen[:m1]), np.sort(chosen[m1:])
+    ok = np.ones(len(K), bool)
+    t = 0
+    for c, nbad in [(c, 1) for c in one] + [(c, 2) for c in two]:
+        for v in rng.choice(per_cert, nbad, replace=False):
+            i = int(c) * per_cert + int(v)
+            corrupt_one(H, S, K, i, t % 8, n_keys, rng)
+            ok[i] = False
+            t += 1
+    return ok, np.sort(chosen), two
 
 
 def certs(n_keys: int, per_cert: int, n_certs: int, seed: int):
