@@ -108,3 +108,49 @@ def test_verify_msg_batch_matches_oracle(pb, oracle_lib):
         want = [oracle_lib.oracle_verify_msg(10, last, d, v, s, g, len(g)) == 1 for v, s, g in cases]
         assert got.tolist() == want
         assert any(want) and not all(want)
+
+
+def _call_args(text: str, start: int) -> list[str]:
+    """Top-level comma-separated arguments of the call whose '(' is at start."""
+    depth, cur, out = 0, "", []
+    for ch in text[start:]:
+        if ch in "([{":
+            depth += 1
+            if depth == 1:
+                continue
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                out.append(cur.strip())
+                break
+        if ch == "," and depth == 1:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    return [a for a in out if a]
+
+
+def test_go_binding_calls_only_header_functions_with_their_arity():
+    """go/pbftv (the cgo package; no Go toolchain here) calls only functions
+    include/pbftv.h declares, each with the header's parameter count."""
+    import glob
+    import re
+    from simple_pbft_amd.pbftv import HEADER_PATH
+    with open(HEADER_PATH) as f:
+        hdr = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    arity = {}
+    for m in re.finditer(r"\b(pbftv_[a-z0-9_]+)\s*\(", hdr):
+        args = _call_args(hdr, m.end() - 1)
+        arity[m.group(1)] = 0 if args == ["void"] else len(args)
+    calls = 0
+    for path in glob.glob(os.path.join(ROOT, "go", "pbftv", "*.go")):
+        with open(path) as f:
+            src = f.read()
+        for m in re.finditer(r"\bC\.(pbftv_[a-z0-9_]+)\(", src):
+            name = m.group(1)
+            assert name in arity, f"{path}: {name} is not in include/pbftv.h"
+            n_args = len(_call_args(src, m.end() - 1))
+            assert n_args == arity[name], f"{path}: {name} called with {n_args} args, header has {arity[name]}"
+            calls += 1
+    assert calls >= 20
