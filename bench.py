@@ -601,6 +601,10 @@ def main():
                          "with --weak: signatures per rank")
     ap.add_argument("--weak", action="store_true", help="weak scaling: every rank verifies its own --n batch")
     ap.add_argument("--keys", type=int, default=100)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="consecutive batches alternate over this many library streams (pbftv_stream_create: each "
+                         "owns its verify scratch), so batch j+1's scalar stage overlaps batch j's comb; 0 = the "
+                         "context's own stream")
     ap.add_argument("--no-extras", action="store_true", help="skip QC latency, host path, CPU baselines, other configs")
     ap.add_argument("--sha-only", action="store_true", help="only configs[4] (SHA-256 digest kernel), one JSON line")
     args = ap.parse_args()
@@ -634,17 +638,31 @@ def main():
     t_reg = time.perf_counter() - t_reg  # G table + one table per key, built on the device
     assert valid.all()
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
-    db = ver.alloc(0, (n + 7) // 8 + 1)
     ver.reserve(n)
+    # one bitmap per stream; batches alternate over the streams (each stream's
+    # verifies are ordered, the streams overlap)
+    streams = [ver.stream_create(0) for _ in range(args.streams)] or [None]
+    dbs = [ver.alloc(0, (n + 7) // 8 + 1) for _ in streams]
+    db = dbs[0]
+    turn = [0]
 
     def step():
         if n:
-            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
+            j = turn[0] % len(streams)
+            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, dbs[j].ptr, stream=streams[j])
+            turn[0] += 1
 
-    step()
-    ver.sync(0)
+    def sync_all():
+        ver.sync(0)
+        for st in streams:
+            if st is not None:
+                ver.stream_wait(0, st)
+
+    for _ in streams:
+        step()
+    sync_all()
     got = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
-    check = bool((got == ok).all())
+    check = all(bool((np.unpackbits(b.to_host(), bitorder="little")[:n].astype(bool) == ok).all()) for b in dbs)
     # Warm-up right before the timed steps, with no idle gap in between: after
     # the GPU idles a few ms the comb needs ~40 ms of load to get back to its
     # steady speed (first step after an 8 ms pause 1.37 ms, then 1.14, 1.24 ...
@@ -655,29 +673,33 @@ def main():
         step()
         w += 1
         if w % 8 == 0:
-            ver.sync(0)  # (the host clock follows the GPU)
+            sync_all()  # (the host clock follows the GPU)
 
     # wall clock over K steps, uninstrumented: a timing event between two
     # kernels costs the GPU a ~6 us gap (rocprof timeline, tools/rocpd_timeline.py)
     d.barrier()
-    ver.sync(0)
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    ver.sync(0)
+    sync_all()
     d.barrier()
     elapsed = time.perf_counter() - t0
     # kernel durations for the roofline: the same K steps again, with HIP events
     # recorded by the library around each scalar / comb launch on its stream
+    # (on ONE stream, so no kernel's event window includes another batch's
+    # overlapping work: these are the kernels' own durations)
     ver.set_kernel_timing(True)
     ver.reset_kernel_times()
     for _ in range(args.steps):
-        step()
-    ver.sync(0)
+        if n:
+            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, dbs[0].ptr, stream=streams[0])
+    sync_all()
     comb_ms, comb_cnt = ver.kernel_time_ms(0, K_ECDSA_COMB)
     scal_ms, scal_cnt = ver.kernel_time_ms(0, K_ECDSA_SCALARS)
     ver.set_kernel_timing(False)
-    check = check and bool((np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool) == ok).all())
+    check = check and all(bool((np.unpackbits(b.to_host(), bitorder="little")[:n].astype(bool) == ok).all())
+                          for b in dbs)
     t_max = d.max(elapsed)
     all_ok = d.sum(0.0 if check else 1.0) == 0.0
     total = n_global * args.steps
@@ -694,7 +716,8 @@ def main():
                                 (f" ({args.n} per rank)" if args.weak else f" sharded N/{ws}") +
                                 f", {args.keys}-key table, 1% corrupted (8 classes)"),
                    "global_batch": n_global, "keys": args.keys,
-                   "parallelism": f"shard{ws} ({mode} scaling: independent per-GPU shards, no collective)"},
+                   "parallelism": f"shard{ws} ({mode} scaling: independent per-GPU shards, no collective)",
+                   "streams": args.streams},
         "check": "pass" if all_ok else "FAIL",
     }
     if rank == 0:
@@ -783,8 +806,11 @@ def main():
                 "n4_3sigs": oc["config2"]["ms"] * 1e3 / oc["config2"]["certs"],
                 "n100_67sigs": oc["config3"]["ms"] * 1e3 / oc["config3"]["certs"]}
         print(json.dumps(out), flush=True)
-    for b in (dh, ds, dk, db):
+    for b in [dh, ds, dk] + dbs:
         b.free()
+    for st in streams:
+        if st is not None:
+            ver.stream_destroy(0, st)
     ver.close()
     d.close()
 

@@ -83,9 +83,14 @@ int pbftv_memset_dev(pbftv_ctx* ctx, int dev, void* dst, int value, uint64_t byt
 /* The context's stream of device dev as a hipStream_t (for *_dev calls). */
 void* pbftv_stream(pbftv_ctx* ctx, int dev);
 int pbftv_stream_sync(pbftv_ctx* ctx, int dev);
-/* Caller streams on device dev for *_dev calls (non-blocking HIP streams).  Device
- * scratch shared by calls on different streams is ordered by the library (an
- * event per device), so concurrent *_dev calls on several streams are safe. */
+/* Caller streams on device dev for *_dev calls (non-blocking HIP streams).  A
+ * stream made here owns its ECDSA verify scratch (stage-1 records, key order,
+ * result bytes; freed by pbftv_stream_destroy), so verifies enqueued on two
+ * such streams run concurrently on the GPU: a caller that alternates batches
+ * between two streams overlaps batch j + 1's scalar stage with batch j's comb.
+ * Other device scratch shared by calls on different streams (d.stream and any
+ * foreign hipStream_t) is ordered by the library (an event per device), so
+ * concurrent *_dev calls on several streams are safe. */
 int pbftv_stream_create(pbftv_ctx* ctx, int dev, void** out_stream);
 int pbftv_stream_destroy(pbftv_ctx* ctx, int dev, void* stream);
 int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);

@@ -162,6 +162,10 @@ struct Device {
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_st = nullptr;
   bool scratch_lazy = false;  // scratch_st == stream: scratch_ev not yet recorded for its last use
+  // streams made by pbftv_stream_create own their verify scratch: ECDSA
+  // verifies on two such streams run concurrently (batch j + 1's scalar stage
+  // in the wave slots batch j's comb leaves free) instead of queueing on d.vs
+  std::map<hipStream_t, std::unique_ptr<VerifyScratch>> stream_scratch;
   // kernel timing (events recorded around launches while ctx timing is on)
   const bool* timing = nullptr;
   static constexpr int kKernels = 5;  // PBFTV_K_*
@@ -535,6 +539,11 @@ void pbftv_close(pbftv_ctx* ctx) {
       (void)hipStreamDestroy(d->stream2);
     }
     d->vs2.release();
+    for (auto& kv : d->stream_scratch) {  // streams the caller did not destroy: their scratch
+      (void)hipStreamSynchronize(kv.first);
+      kv.second->release();
+    }
+    d->stream_scratch.clear();
     if (d->join_ev) (void)hipEventDestroy(d->join_ev);
     d->keys_all.release();
     if (d->cstream) {
@@ -647,6 +656,10 @@ int pbftv_stream_create(pbftv_ctx* ctx, int dev, void** out_stream) {
   HIP_TRY(hipSetDevice(d->id));
   hipStream_t st;
   HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  {
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->stream_scratch[st] = std::make_unique<VerifyScratch>();
+  }
   *out_stream = reinterpret_cast<void*>(st);
   return PBFTV_OK;
 }
@@ -655,8 +668,17 @@ int pbftv_stream_destroy(pbftv_ctx* ctx, int dev, void* stream) {
   Device* d = dev_of(ctx, dev);
   if (!d || !stream) return fail(PBFTV_EINVAL, "bad context, device index or stream");
   HIP_TRY(hipSetDevice(d->id));
-  HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
-  HIP_TRY(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(hipStreamSynchronize(st));
+  {
+    std::lock_guard<std::mutex> lk(d->mu);
+    auto it = d->stream_scratch.find(st);
+    if (it != d->stream_scratch.end()) {
+      it->second->release();
+      d->stream_scratch.erase(it);
+    }
+  }
+  HIP_TRY(hipStreamDestroy(st));
   return PBFTV_OK;
 }
 
@@ -1054,6 +1076,10 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
                                       d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), d_bitmap, nullptr, st);
     }));
     return PBFTV_OK;
+  }
+  if (!own) {
+    auto it = d.stream_scratch.find(st);
+    if (it != d.stream_scratch.end()) own = it->second.get();
   }
   VerifyScratch& sc = own ? *own : d.vs;
   HIP_TRY(sc.rec.ensure(pbftv::ecdsa_record_bytes(n)));
