@@ -474,6 +474,16 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
   // pass, where Go's remaining checks decide the record's ok.
   fe acc, rk;
   uint32_t okm = 0;  // bit j: 0 < s_j < n
+  // K <= 2 (the small strong-scaling shards, one wave round): every input of
+  // the lane's signatures is loaded here, so its HBM latency hides behind the
+  // forward products and the inversion instead of sitting on the backward
+  // pass's chain (~52 more VGPRs at K = 2, still 2 waves per SIMD)
+  constexpr bool kPre = K <= 2;
+  constexpr int KP = kPre ? K : 1;
+  uint32_t pr[KP][8], ps[KP][8], pe[KP][8], pk[KP];
+  bool pv[KP];
+  constexpr int KU = kPre ? K : 1;  // fully unrolled with the prefetch (register arrays, no scratch)
+#pragma unroll KU
   for (int j = 0; j < K; ++j) {
     const uint64_t i = lane + (uint64_t)j * L;
     uint32_t sw[8] = {1, 0, 0, 0, 0, 0, 0, 0};
@@ -481,10 +491,18 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
     if (i < n) {
       uint32_t s[8];
       load_be256(sigs + 64 * i + 32, s);
+      uint32_t k;
+      if constexpr (kPre) {
+        load_be256(sigs + 64 * i, pr[j]);
+        load_be256(hashes + 32 * i, pe[j]);
+        k = pk[j] = key_idx[i];
+        pv[j] = k < nkeys && key_valid[k] != 0;
+        PBFTV_UNROLL for (int t = 0; t < 8; ++t) ps[j][t] = s[t];
+      }
       oks = !words_is_zero(s) && words_lt(s, kN32);
       if (oks) PBFTV_UNROLL for (int t = 0; t < 8; ++t) sw[t] = s[t];
       if (sorted) {
-        const uint32_t k = key_idx[i];
+        if constexpr (!kPre) k = key_idx[i];
         atomicAdd(&kh[k < nk ? k : nk], 1u);  // bin nk: out-of-range key indices (rejected below)
       }
     }
@@ -516,6 +534,7 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
     fe_set(rk, kRPowN[K]);
     fn_mul(inv, inv, rk);      // P^-1 R^K
   }
+#pragma unroll KU
   for (int j = K - 1; j >= 0; --j) {
     const uint64_t i = lane + (uint64_t)j * L;
     const bool oks = (okm >> j) & 1u;
@@ -523,7 +542,15 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
     bool ok = false;
     if (i < n) {
       uint32_t sl[8];
-      ok = oks && sig_ok(sigs, key_idx, key_valid, nkeys, i, r, sl);  // Go's range checks + a valid key
+      if constexpr (kPre) {  // Go's range checks + a valid key on the prefetched inputs
+        PBFTV_UNROLL for (int t = 0; t < 8; ++t) {
+          r[t] = pr[j][t];
+          sl[t] = ps[j][t];
+        }
+        ok = oks && pv[j] && !words_is_zero(r) && words_lt(r, kN32);
+      } else {
+        ok = oks && sig_ok(sigs, key_idx, key_valid, nkeys, i, r, sl);  // Go's range checks + a valid key
+      }
       if (oks) PBFTV_UNROLL for (int t = 0; t < 8; ++t) s[t] = sl[t];
     }
     if (!ok) PBFTV_UNROLL for (int t = 0; t < 8; ++t) r[t] = 0;
@@ -546,7 +573,11 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
       uint32_t u1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, u2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       if (ok) {
         uint32_t e[8];
-        load_be256(hashes + 32 * i, e);
+        if constexpr (kPre) {
+          PBFTV_UNROLL for (int t = 0; t < 8; ++t) e[t] = pe[j][t];
+        } else {
+          load_be256(hashes + 32 * i, e);
+        }
         fe ev, rv, t;
         fe_from_words(ev, e);
         fe_from_words(rv, r);
@@ -558,10 +589,10 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
         fe_to_words(u2, t);
       }
       uint64_t at = i;
-      if (sorted) {
-        const uint32_t k = key_idx[i];
-        at = atomicAdd(&kh[k < nk ? k : nk], 1u);  // the signature's place in key order
-      }
+      uint32_t kj;
+      if constexpr (kPre) kj = pk[j];
+      else kj = key_idx[i];
+      if (sorted) at = atomicAdd(&kh[kj < nk ? kj : nk], 1u);  // the signature's place in key order
       SigRec* o = rec + at;
       o->q[0] = make_uint4(u1[0], u1[1], u1[2], u1[3]);
       o->q[1] = make_uint4(u1[4], u1[5], u1[6], u1[7]);
@@ -569,7 +600,7 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
       o->q[3] = make_uint4(u2[4], u2[5], u2[6], u2[7]);
       o->q[4] = make_uint4(r[0], r[1], r[2], r[3]);
       o->q[5] = make_uint4(r[4], r[5], r[6], r[7]);
-      o->q[6] = make_uint4(ok ? key_idx[i] : 0u, (uint32_t)i, ok ? 1u : 0u, 0u);
+      o->q[6] = make_uint4(ok ? kj : 0u, (uint32_t)i, ok ? 1u : 0u, 0u);
     }
   }
 }

@@ -627,8 +627,99 @@ __device__ __forceinline__ int32_t lane_from_prev(int32_t x) {  // lane j <- lan
 __device__ __forceinline__ int32_t center30(uint32_t x) { return (int32_t)(x << 2) >> 2; }
 
 // divsteps30_var (safegcd.h) shaped for the scalar unit, where every
-// instruction of the one wave costs an issue slot: -f^-1 mod 64 is recomputed
-// only when f changes (a swap), and the loop tests its exit at the bottom.
+// instruction of the one wave costs an issue slot (a lone wave issues one
+// instruction per ~4 cycles, so the inversion's latency is its instruction
+// count): -f^-1 mod 64 is recomputed only when f changes (a swap).
+//
+// Hand-scheduled SALU (PBFTV_DIVSTEP_ASM, the default; the C++ form below is
+// the reference and the fallback): per elimination step 24 instructions
+// (the compiler's form: ~32, five of them register moves the swap's phi
+// nodes forced on the no-swap path).  The swap moves no register: the loop
+// exists twice, with (f, g), (u, q), (v, r) in exchanged registers, and a
+// swap negates three registers in place and continues in the other copy.
+//   z = min(ctz(g), i)             s_ff1 (-1 for g == 0) + s_min_u32
+//   w = (g nfi) & bfm(min(eta + 1, i, 6))   (the same mask as the C++ form)
+// Scalar ALU only: no scalar memory access of any kind.
+#ifndef PBFTV_DIVSTEP_ASM
+#define PBFTV_DIVSTEP_ASM 1
+#endif
+#if PBFTV_DIVSTEP_ASM
+#define PBFTV_DS_STEP(F, G, U, V, Q, R, EXIT)                                                            \
+  "s_ff1_i32_b32 %[z], " G "\n"                                                                          \
+  "s_min_u32 %[z], %[z], %[i]\n"                                                                         \
+  "s_lshr_b32 " G ", " G ", %[z]\n"                                                                      \
+  "s_lshl_b32 " U ", " U ", %[z]\n"                                                                      \
+  "s_lshl_b32 " V ", " V ", %[z]\n"                                                                      \
+  "s_sub_i32 %[eta], %[eta], %[z]\n"                                                                     \
+  "s_sub_u32 %[i], %[i], %[z]\n"                                                                         \
+  "s_cmp_eq_u32 %[i], 0\n"                                                                               \
+  "s_cbranch_scc1 " EXIT "\n"
+#define PBFTV_DS_ELIM(F, G, U, V, Q, R)                                                                  \
+  "s_add_i32 %[m], %[eta], 1\n"                                                                          \
+  "s_min_u32 %[m], %[m], %[i]\n"                                                                         \
+  "s_min_u32 %[m], %[m], 6\n"                                                                            \
+  "s_bfm_b32 %[m], %[m], 0\n"                                                                            \
+  "s_mul_i32 %[w], " G ", %[nfi]\n"                                                                      \
+  "s_and_b32 %[w], %[w], %[m]\n"                                                                         \
+  "s_mul_i32 %[m], " F ", %[w]\n"                                                                        \
+  "s_add_u32 " G ", " G ", %[m]\n"                                                                       \
+  "s_mul_i32 %[m], " U ", %[w]\n"                                                                        \
+  "s_add_u32 " Q ", " Q ", %[m]\n"                                                                       \
+  "s_mul_i32 %[m], " V ", %[w]\n"                                                                        \
+  "s_add_u32 " R ", " R ", %[m]\n"
+// swap: (f, g, u, v, q, r, eta) <- (g, -f, q, r, -u, -v, -eta), in place: the
+// registers of f, u, v now hold -f, -u, -v = the new g, q, r
+#define PBFTV_DS_SWAP(F, G, U, V)                                                                        \
+  "s_sub_i32 %[eta], 0, %[eta]\n"                                                                        \
+  "s_sub_u32 " F ", 0, " F "\n"                                                                          \
+  "s_sub_u32 " U ", 0, " U "\n"                                                                          \
+  "s_sub_u32 " V ", 0, " V "\n"                                                                          \
+  "s_mul_i32 %[w], " G ", " G "\n"                                                                       \
+  "s_add_i32 %[w], %[w], -2\n"                                                                           \
+  "s_mul_i32 %[nfi], %[w], " G "\n"
+
+__device__ __forceinline__ int32_t divsteps30_scalar(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1, i = 30, z, w, m;
+  uint32_t nfi = f * (f * f - 2u);  // -f^-1 mod 64 (Newton step from f f = 1 mod 8)
+  // copy A: (f, g, u, v, q, r) in their own registers; copy B: exchanged
+  asm volatile(
+      "s_branch .LdsA1_%=\n"
+      ".LdsA3_%=:\n" PBFTV_DS_ELIM("%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]")
+      ".LdsA1_%=:\n" PBFTV_DS_STEP("%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]", ".LdsXA_%=")
+      "s_cmp_lt_i32 %[eta], 0\n"
+      "s_cbranch_scc0 .LdsA3_%=\n"
+      PBFTV_DS_SWAP("%[f]", "%[g]", "%[u]", "%[v]")
+      ".LdsB3_%=:\n" PBFTV_DS_ELIM("%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]")
+      PBFTV_DS_STEP("%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]", ".LdsXB_%=")
+      "s_cmp_lt_i32 %[eta], 0\n"
+      "s_cbranch_scc0 .LdsB3_%=\n"
+      PBFTV_DS_SWAP("%[g]", "%[f]", "%[q]", "%[r]")
+      "s_branch .LdsA3_%=\n"
+      ".LdsXB_%=:\n"  // ended in copy B: back to copy A's registers
+      "s_mov_b32 %[w], %[f]\n"
+      "s_mov_b32 %[f], %[g]\n"
+      "s_mov_b32 %[g], %[w]\n"
+      "s_mov_b32 %[w], %[u]\n"
+      "s_mov_b32 %[u], %[q]\n"
+      "s_mov_b32 %[q], %[w]\n"
+      "s_mov_b32 %[w], %[v]\n"
+      "s_mov_b32 %[v], %[r]\n"
+      "s_mov_b32 %[r], %[w]\n"
+      ".LdsXA_%=:\n"
+      : [f] "+s"(f), [g] "+s"(g), [u] "+s"(u), [v] "+s"(v), [q] "+s"(q), [r] "+s"(r), [eta] "+s"(eta),
+        [i] "+s"(i), [nfi] "+s"(nfi), [z] "=&s"(z), [w] "=&s"(w), [m] "=&s"(m)
+      :
+      : "scc");
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return eta;
+}
+#undef PBFTV_DS_STEP
+#undef PBFTV_DS_ELIM
+#undef PBFTV_DS_SWAP
+#else
 __device__ __forceinline__ int32_t divsteps30_scalar(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
   uint32_t nfi = f * (f * f - 2u);  // -f^-1 mod 64 (Newton step from f f = 1 mod 8)
@@ -665,6 +756,7 @@ __device__ __forceinline__ int32_t divsteps30_scalar(int32_t eta, uint32_t f, ui
   t.r = (int32_t)r;
   return eta;
 }
+#endif
 
 // limb re-centering: carry (x + 2^29) >> 30 one lane up (not out of the top limb)
 __device__ __forceinline__ int32_t limbs_center(int32_t x, bool top) {

@@ -3,10 +3,11 @@
 #   bash tools/streams_ab.sh OUT ROUNDS "N STREAMS [ENV=V ...]" ...  -> OUT/summary.txt
 set -euo pipefail
 OUT=$1; ROUNDS=$2; shift 2
+VARIANTS=("$@")
 mkdir -p "$OUT"
 for r in $(seq 1 "$ROUNDS"); do
   i=0
-  for v in "$@"; do
+  for v in "${VARIANTS[@]}"; do
     set -- $v
     N=$1; S=$2; shift 2
     f="$OUT/r${r}_${i}.json"
