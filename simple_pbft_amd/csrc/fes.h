@@ -228,4 +228,30 @@ PBFTV_HD void xyzz_madd_s(xyzz_s& acc, const fe& x2, const fe& y2) {
   acc.x = x3;
 }
 
+// The same addition with the accumulator's Y kept as W = sigma Y (sigma = +-1,
+// a per-lane sign the caller tracks) and the result returned with the OTHER
+// sign: for W1 = sigma Y1 and y2 given as sigma y2,
+//   R' = sigma y2 ZZZ1 - W1 = sigma R            (R'^2 = R^2: X3 unchanged)
+//   -sigma Y3 = -sigma R (Q - X3) + sigma Y1 PPP = R' (X3 - Q) + W1 PPP,
+// so Y3 needs no negation of Y1 (xyzz_madd_s's fs_neg: 9 VALU per addition).
+// Callers flip sigma after every addition; X, ZZ and ZZZ are sign-free, and the
+// comb's x-coordinate check never reads Y.
+PBFTV_HD void xyzz_madd_s_flip(xyzz_s& acc, const fe& x2, const fe& y2) {
+  fe u2, s2, p, r, pp, ppp, q, t;
+  fs_mul(u2, x2, acc.zz);
+  fs_mul(s2, y2, acc.zzz);
+  fs_sub(p, u2, acc.x);                // P = U2 - X1            D
+  fs_sub(r, s2, acc.y);                // R' = sigma R           D
+  fs_sqr(pp, p);
+  fs_mul(ppp, p, pp);
+  fs_mul(q, acc.x, pp);
+  fe x3;
+  fs_sqr_sub2(x3, r, ppp, q);          // X3 = R^2 - PPP - 2Q    S
+  fs_sub(t, x3, q);                    // X3 - Q                 D
+  fs_mul2_add(acc.y, r, t, acc.y, ppp);  // -sigma Y3 = R' (X3 - Q) + W1 PPP, one reduction
+  fs_mul(acc.zz, acc.zz, pp);          // ZZ3 = ZZ1 PP
+  fs_mul(acc.zzz, acc.zzz, ppp);       // ZZZ3 = ZZZ1 PPP
+  acc.x = x3;
+}
+
 }  // namespace pbftv

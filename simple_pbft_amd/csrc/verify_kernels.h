@@ -244,8 +244,8 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
       sdig[j][t] = (typename S::Digit)((S::is_q(j) ? s2.next() : s1.next()) - 1);
   }
   const uint4* qtab = act ? qtabs[meta.x] : gtab;  // the key's own table allocation
-  xyzz_s R;  // signed-limb accumulator (fes.h)
-  bool inf = true;
+  xyzz_s R;  // signed-limb accumulator (fes.h); R.y holds sigma Y (xyzz_madd_s_flip)
+  bool inf = true, neg_y = false;  // neg_y: sigma = -1
   int d = (int)sdig[0][t] + 1;
   issue_entry_lds(sent, t, entry_ptr<WG>(gtab, 0, d));
 #pragma unroll 1
@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
     if (dc != 0) {
       fe x, y;
       entry_to_fe(x, y, w16);
-      fs_cneg(y, y, dc < 0);  // negative digit: -y, D-type (no carry chain)
+      fs_cneg(y, y, (dc < 0) != neg_y);  // sigma * (+-y): D-type (no carry chain)
       if (inf) {
         R.x = x;
         fs_norm(R.y, y);
@@ -269,7 +269,8 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
         fe_set(R.zzz, kOneP);
         inf = false;
       } else {
-        xyzz_madd_s(R, x, y);
+        xyzz_madd_s_flip(R, x, y);  // Y3 comes back with the other sign
+        neg_y = !neg_y;
       }
     }
   }

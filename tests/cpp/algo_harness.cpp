@@ -220,6 +220,15 @@ void h_xyzz_madd_s(uint32_t* acc, const uint32_t* pt) {
   memcpy(acc, A.x.v, 36); memcpy(acc + 9, A.y.v, 36); memcpy(acc + 18, A.zz.v, 36); memcpy(acc + 27, A.zzz.v, 36);
 }
 
+void h_xyzz_madd_s_flip(uint32_t* acc, const uint32_t* pt) {
+  xyzz_s A;
+  fe x, y;
+  memcpy(A.x.v, acc, 36); memcpy(A.y.v, acc + 9, 36); memcpy(A.zz.v, acc + 18, 36); memcpy(A.zzz.v, acc + 27, 36);
+  memcpy(x.v, pt, 36); memcpy(y.v, pt + 9, 36);
+  xyzz_madd_s_flip(A, x, y);
+  memcpy(acc, A.x.v, 36); memcpy(acc + 9, A.y.v, 36); memcpy(acc + 18, A.zz.v, 36); memcpy(acc + 27, A.zzz.v, 36);
+}
+
 // XYZZ mixed addition on raw limbs: acc = x||y||zz||zzz (36 words), pt = x||y (18 words).
 void h_xyzz_madd(uint32_t* acc, const uint32_t* pt) {
   xyzz A;

@@ -438,6 +438,54 @@ def test_xyzz_madd_s_chain_values_and_bounds(H):
         assert sval(a2[18:27]) % P == 0 and sval(a2[27:36]) % P == 0
 
 
+def test_xyzz_madd_s_flip_chain(H):
+    """The comb's sign-alternating step (xyzz_madd_s_flip, verify_kernels.h
+    k_ecdsa_comb): the accumulator holds W = sigma Y, the point is passed as
+    sigma (+-y), sigma flips after every addition.  200 steps with random
+    digit signs: sigma W equals the big-integer sum's Y at every step, X / ZZ /
+    ZZZ equal it outright, every coordinate stays S-type, and an addition that
+    meets the point (or its negative) leaves ZZ == ZZZ == 0."""
+    from oracle import p256
+    rng = np.random.default_rng(72)
+    A = ctypes.c_uint32 * 36
+    Pt = ctypes.c_uint32 * 18
+
+    def mont(v):
+        return v * R % P
+
+    def unmont(v):
+        return v * pow(R, -1, P) % P
+
+    def from_acc(acc, sigma):
+        x, w, zz, zzz = (unmont(sval(acc[9 * k:9 * k + 9]) % P) for k in range(4))
+        assert zz != 0 and zzz != 0
+        return x * pow(zz, -1, P) % P, sigma * w * pow(zzz, -1, P) % P
+
+    cur = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+    acc = A(*[w for v in (mont(cur[0]), mont(cur[1]), mont(1), mont(1)) for w in limbs(v)])
+    sigma = 1
+    for step in range(200):
+        q = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+        neg = bool(rng.integers(0, 2))
+        flip = neg != (sigma == -1)  # the kernel's (dc < 0) != neg_y
+        ly = [(-x) & 0xFFFFFFFF if flip else x for x in limbs(mont(q[1]))]
+        H.h_xyzz_madd_s_flip(acc, Pt(*limbs(mont(q[0])), *ly))
+        sigma = -sigma
+        if neg:
+            q = (q[0], (P - q[1]) % P)
+        cur = p256.point_add(cur, q)
+        assert from_acc(acc, sigma) == cur, step
+        for k in range(4):
+            check_s(acc[9 * k:9 * k + 9])
+    for neg in (False, True):
+        x, y = from_acc(acc, sigma)
+        y = (P - y) % P if neg else y
+        ys = (P - y) % P if sigma == -1 else y
+        a2 = A(*acc)
+        H.h_xyzz_madd_s_flip(a2, Pt(*limbs(mont(x)), *limbs(mont(ys))))
+        assert sval(a2[18:27]) % P == 0 and sval(a2[27:36]) % P == 0
+
+
 # ---- lane-parallel safegcd of the latency path (verify_kernels.h inv_mod_n_wave) ----
 # A restatement of the kernel's scheme with exact integers: one list entry per
 # lane-limb, 30-bit signed limbs re-centered after every batch, divsteps on the
