@@ -420,17 +420,16 @@ __device__ __forceinline__ void quad_mul(fe& p, int role, const fe& a0, const fe
   fs_mul(p, a, b);  // signed-limb product (fes.h): operands S- or D-type
 }
 
-// (gx, gy) + (qx, qy), both affine S-type, into XYZZ (mmadd-2008-s, 3 steps);
-// exc if the x-coordinates meet.  Signed-limb arithmetic (fes.h): differences
+// (gx, gy) + (qx, qy), both affine S-type, into XYZZ (mmadd-2008-s, 3 steps).  Signed-limb arithmetic (fes.h): differences
 // are D-type, X3 is renormalised (S), Y3 stays D-type (only multiplied later).
 // The idle lane of step 3 computes rz = rm ZZ3 (r ZZ in Montgomery form, for
 // the fused check of the last level).
-__device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, fe& rz, bool& exc, int role, const fe& gx, const fe& gy,
+__device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, fe& rz, int role, const fe& gx, const fe& gy,
                                                 const fe& qx, const fe& qy, const fe& rm) {
   fe p, rr, pp, r2, ppp, qq, x3, t, a, b, prod;
   fs_sub(p, qx, gx);
   fs_sub(rr, qy, gy);
-  exc = fs_is_zero(p);
+  // (x-coordinates meeting: PP = 0 = ZZ3, tested at the top of the tree)
   quad_mul(prod, role, p, p, rr, rr, p, p, rr, rr);          // PP, R^2
   quad_bcast<0>(pp, prod);
   quad_bcast<1>(r2, prod);
@@ -455,8 +454,8 @@ __device__ __forceinline__ void quad_mmadd_xyzz(xyzz_s& r, fe& rz, bool& exc, in
 // x-coordinates meet (P == 0).  The idle lane of step 4 computes rz = rm ZZ
 // of the level's result: of r, or of Q / P when the other side is infinity
 // (pinf / qinf), so r ZZ needs no shuffle of its own.
-__device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, fe& rz, bool& exc, int role, const xyzz_s& P,
-                                              const xyzz_s& Q, const fe& rm, bool pinf, bool qinf) {
+__device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, fe& rz, int role, const xyzz_s& P, const xyzz_s& Q,
+                                              const fe& rm, bool qinf) {
   fe prod, u1, u2, s1, s2, p, rr, pp, r2, zz12, zzz12, ppp, qq, x3, t, a, b;
   quad_mul(prod, role, P.x, Q.zz, Q.x, P.zz, P.y, Q.zzz, Q.y, P.zzz);      // U1, U2, S1, S2
   quad_bcast<0>(u1, prod);
@@ -464,8 +463,7 @@ __device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, fe& rz, bool& exc, int 
   quad_bcast<2>(s1, prod);
   quad_bcast<3>(s2, prod);
   fs_sub(p, u2, u1);
-  fs_sub(rr, s2, s1);
-  exc = fs_is_zero(p);
+  fs_sub(rr, s2, s1);  // (P == 0 -- a doubling or cancellation -- leaves ZZ3 = 0: the caller tests ZZ once)
   quad_mul(prod, role, p, p, rr, rr, P.zz, Q.zz, P.zzz, Q.zzz);             // PP, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2
   quad_bcast<0>(pp, prod);
   quad_bcast<1>(r2, prod);
@@ -479,7 +477,7 @@ __device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, fe& rz, bool& exc, int 
   fs_norm(x3, x3);                                                          // X3 = R^2 - PPP - 2Q
   fs_sub(t, qq, x3);
   fe zsel;
-  fe_sel3(zsel, pinf, Q.zz, qinf, P.zz, r.zz);
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) zsel.v[l] = qinf ? P.zz.v[l] : r.zz.v[l];  // the ZZ the quad keeps
   quad_mul(prod, role, rr, t, s1, ppp, zzz12, ppp, rm, zsel);               // R (Q - X3), S1 PPP, ZZZ3, r ZZ
   quad_bcast<0>(a, prod);
   quad_bcast<1>(b, prod);
@@ -493,7 +491,10 @@ __device__ __forceinline__ void quad_xyzz_add(xyzz_s& r, fe& rz, bool& exc, int 
 // with r afterwards): with rz = r ZZ1 from the previous level,
 //   X3 == r ZZ3  <=>  R^2 - PP (P + 2 U1) == (r ZZ1) ZZ2 PP  <=>  R^2 == PP (P + 2 U1 + rz ZZ2),
 // three steps instead of four plus one.  Only for the test against r (the
-// caller takes the full path when r + n < p also has to be tried).
+// caller takes the full path when r + n < p also has to be tried).  exc: this
+// level's P == 0, or r ZZ1 ZZ2 == 0 -- i.e. ZZ1 ZZ2 == 0 (0 < r < n < p): an
+// exceptional addition anywhere below left a zero ZZ, which every later
+// product keeps (one test for the whole tree).
 __device__ __forceinline__ bool quad_xyzz_add_check(bool& exc, int role, const xyzz_s& P, const xyzz_s& Q,
                                                     const fe& rz) {
   fe prod, u1, u2, s1, s2, p, rr, pp, r2, rz12, w, t, d;
@@ -509,6 +510,7 @@ __device__ __forceinline__ bool quad_xyzz_add_check(bool& exc, int role, const x
   quad_bcast<0>(pp, prod);
   quad_bcast<1>(r2, prod);
   quad_bcast<2>(rz12, prod);
+  exc = exc || fs_is_zero(rz12);
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) w.v[i] = (u1.v[i] << 1) + rz12.v[i];
   fs_norm(w, w);
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) w.v[i] += p.v[i];                // P + 2 U1 + r ZZ12: |limbs| < 2^30
@@ -518,6 +520,39 @@ __device__ __forceinline__ bool quad_xyzz_add_check(bool& exc, int role, const x
 }
 
 __device__ __forceinline__ bool wave_check(const xyzz_s& P, bool finite, const fe& rm, const fe& rnm, bool rn_ok);
+
+// Signed digit of window q (this lane's quad) of a uniform 256-bit scalar u,
+// equal to the q-th digit_stream<W>::next() -- without walking the lower
+// windows: the lane cuts its window's raw bits out of u (a funnel shift of the
+// two words it spans), and the recoding carries come from one wave-wide
+// carry-lookahead on ballots: window k generates a carry when raw_k > 2^(w-1)
+// and propagates the incoming one when raw_k == 2^(w-1), so with G / P those
+// masks at bit 4k (lane 4k of each quad) and bits 4k+1..4k+3 set to
+// "propagate", the carries into every window are (G + (G|P)) ^ G ^ (G|P), one
+// 64-bit add (~30 instructions per scalar instead of the ~130 of stepping the
+// 256-bit shift through the lower windows).  Every lane of the wave must call it.
+template <int W>
+__device__ __forceinline__ int lane_window_digit(const uint32_t u[8], int q) {
+  using Gm = CombGeom<W>;
+  const bool valid = q < Gm::kWin;
+  const int qq = valid ? q : 0;
+  const int bit = Gm::bit(qq), wd = Gm::width(qq);
+  const int wi = bit >> 5, sh = bit & 31;
+  uint32_t lo = 0, hi = 0;
+  PBFTV_UNROLL for (int k = 0; k < 8; ++k) {
+    lo = wi == k ? u[k] : lo;
+    hi = wi + 1 == k ? u[k] : hi;
+  }
+  uint32_t raw = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh) & ((1u << wd) - 1u);
+  if (!valid) raw = 0;
+  const uint32_t half = 1u << (wd - 1);
+  constexpr uint64_t kQuad0 = 0x1111111111111111ull;
+  const uint64_t G = __ballot(raw > half) & kQuad0;
+  const uint64_t B = G | (__ballot(raw == half) & kQuad0) | ~kQuad0;
+  const uint64_t C = (G + B) ^ G ^ B;  // carry into every bit
+  const int d = (int)raw + (int)((C >> (4 * q)) & 1u);
+  return d - ((d > (int)half ? 1 : 0) << wd);
+}
 
 // quad q = window q: G entry + Q entry, then a butterfly over the quads; the
 // last level fused with the check against r (quad_xyzz_add_check) unless
@@ -532,15 +567,7 @@ __device__ __forceinline__ bool wave_verify_quads(bool& exc, const uint32_t u1[8
   constexpr int nW = nG > nQ ? nG : nQ;
   static_assert(nW > 8 && nW <= 16, "one quad per window, four butterfly levels");
   const int role = threadIdx.x & 3, q = threadIdx.x >> 2;
-  digit_stream<WG> s1;
-  digit_stream<WQ> s2;
-  PBFTV_UNROLL for (int k = 0; k < 8; ++k) { s1.w[k] = u1[k]; s2.w[k] = u2[k]; }
-  s1.carry = s2.carry = 0;
-  int d1 = 0, d2 = 0;
-  for (int k = 0; k < nW; ++k) {
-    const int a = k < nG ? s1.next() : 0, b = k < nQ ? s2.next() : 0;
-    if (k == q) { d1 = a; d2 = b; }
-  }
+  const int d1 = lane_window_digit<WG>(u1, q), d2 = lane_window_digit<WQ>(u2, q);
   uint4 eg[4], eq[4];
   uint32_t w16[16];
   load_entry<WG>(gtab, q < nG ? q : 0, d1, eg);
@@ -556,10 +583,12 @@ __device__ __forceinline__ bool wave_verify_quads(bool& exc, const uint32_t u1[8
   fs_norm(qy, qy);
   xyzz_s S, P;
   fe rz, rzS;
-  bool e0;
-  quad_mmadd_xyzz(S, rzS, e0, role, gx, gy, qx, qy, rm);  // every quad runs it; selected below
-  exc = d1 != 0 && d2 != 0 && e0;
-  bool inf = d1 == 0 && d2 == 0;
+  quad_mmadd_xyzz(S, rzS, role, gx, gy, qx, qy, rm);  // every quad runs it; selected below
+  // A window with two zero digits (probability ~2^-50) would be an infinite
+  // partial sum inside the tree: left to the exact rerun.  (A level-0 meeting,
+  // P == 0, leaves S.zz = PP = 0 and is caught by the ZZ test at the top.)
+  const bool live = q < nW;  // quads past the last window hold no point
+  bool rare = live && d1 == 0 && d2 == 0;
   const bool both = d1 != 0 && d2 != 0, g_only = d1 != 0;
   fe one;
   fe_set(one, kOneP);
@@ -568,6 +597,14 @@ __device__ __forceinline__ bool wave_verify_quads(bool& exc, const uint32_t u1[8
   fe_sel3(P.zz, both, S.zz, true, one, one);
   fe_sel3(P.zzz, both, S.zzz, true, one, one);
   fe_sel3(rz, both, rzS, true, rm, rm);  // a lone table point: ZZ = 1, r ZZ = rm
+  // Butterfly over the quads.  Only quad 0's result is read (its lanes report
+  // the verdict), and the partial sums it depends on are those of the quads
+  // that are multiples of 2m at level m, each adding quad q + m.  For those a
+  // partner past the last window (q + m >= nW) is the point at infinity --
+  // known statically -- and the quad keeps its sum; the partner of a live
+  // quad is never live-but-infinite (rare windows go to the rerun), so no
+  // infinity flags travel and the only select is "keep or take the sum".
+  // The other quads compute don't-care values.
 #pragma unroll 1
   for (int m = 1; m < 16; m <<= 1) {
     xyzz_s Q;
@@ -575,31 +612,23 @@ __device__ __forceinline__ bool wave_verify_quads(bool& exc, const uint32_t u1[8
     shfl_xor_fe(Q.y, P.y, 4 * m);
     shfl_xor_fe(Q.zz, P.zz, 4 * m);
     shfl_xor_fe(Q.zzz, P.zzz, 4 * m);
-    const bool qinf = __shfl_xor((int)inf, 4 * m, 64) != 0;
-    bool e;
-    if (m == 8 && !rn_ok) {  // last level, fused with the check (rn_ok is wave-uniform)
-      bool ok;
-      e = false;
-      if (inf || qinf) {     // a lone partial sum (quad-uniform branch): its own X == r ZZ
-        fe d, rzq;
-        if (inf) fs_mul(rzq, rm, Q.zz);
-        fs_sub(d, inf ? Q.x : P.x, inf ? rzq : rz);
-        ok = !(inf && qinf) && fs_is_zero(d);
-      } else {
-        ok = quad_xyzz_add_check(e, role, P, Q, rz);
-      }
-      exc = exc || (e && !inf && !qinf);
+    const bool qinf = (q ^ m) >= nW;
+    if (m == 8 && !rn_ok) {  // last level, fused with the check (rn_ok is wave-uniform); quad 8 < nW is live
+      bool e = false;
+      const bool ok = quad_xyzz_add_check(e, role, P, Q, rz);
+      exc = __any(rare || (q == 0 && e));
       return ok;
     }
-    quad_xyzz_add(S, rz, e, role, P, Q, rm, inf, qinf);
-    exc = exc || (e && !inf && !qinf);
-    fe_sel3(P.x, inf, Q.x, qinf, P.x, S.x);
-    fe_sel3(P.y, inf, Q.y, qinf, P.y, S.y);
-    fe_sel3(P.zz, inf, Q.zz, qinf, P.zz, S.zz);
-    fe_sel3(P.zzz, inf, Q.zzz, qinf, P.zzz, S.zzz);
-    inf = inf && qinf;
+    quad_xyzz_add(S, rz, role, P, Q, rm, qinf);
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+      P.x.v[l] = qinf ? P.x.v[l] : S.x.v[l];
+      P.y.v[l] = qinf ? P.y.v[l] : S.y.v[l];
+      P.zz.v[l] = qinf ? P.zz.v[l] : S.zz.v[l];
+      P.zzz.v[l] = qinf ? P.zzz.v[l] : S.zzz.v[l];
+    }
   }
-  return wave_check(P, !inf, rm, rnm, rn_ok);
+  exc = __any(rare || (q == 0 && fs_is_zero(P.zz)));  // r + n < p: the full sum, its ZZ tested once
+  return wave_check(P, true, rm, rnm, rn_ok);
 }
 
 // ---- latency-path scalars: the inversion spread over the wave --------------
@@ -987,11 +1016,11 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
       r[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[k]);
       s[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[k]);
     }
+    const uint4* qtab = qtabs[key_idx[i]];  // (loaded now: ready when the scalars are)
     uint32_t u1[8], u2[8];
     fe rm, rnm;
     bool rn_ok;
     wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
-    const uint4* qtab = qtabs[key_idx[i]];
     bool inf;
     bool exc = true;
     if constexpr (nW > 8 && nW <= 16) {
