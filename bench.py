@@ -8,7 +8,12 @@ Workload (BASELINE.json configs[3]): 1,048,576
 signatures per rank over a 100-key table, 1 % corrupted evenly across the 8
 corruption classes; synthetic (OpenSSL-signed, tools/synth.py).  One "step" =
 one pass of the verify path (scalar kernel + comb kernel) over the rank's
-whole batch, inputs already resident in HBM.  Multi-GPU: one process per GPU,
+whole batch, inputs already resident in HBM.  Consecutive steps alternate
+over two library streams (--streams 2, pbftv_stream_create: each owns its
+verify scratch), as a node flushing pool snapshots back to back would: step
+j + 1's scalar stage runs in the wave slots step j's comb leaves free.  Every
+step is still a complete verify of the batch, checked against the
+construction; --streams 0 queues every step on one stream.  Multi-GPU: one process per GPU,
 each verifying its own shard -- no collective on the data path; torch.distributed
 (gloo, CPU) is used only for the barrier and the max-over-ranks time, so torch
 never touches the GPU (it bundles its own HIP runtime).
@@ -82,7 +87,13 @@ def macs_comb(gbits: int, qbits: int) -> float:
 INV_N_MACS = 25 * (36 + 54) + 162
 
 
-GATHER_ONLY_TBPS = 1.2  # 21 random 64-B gathers per lane over 1M lanes, no arithmetic (gather_calib)
+# the comb's table reads alone, in the comb's own pattern (key-ordered lanes,
+# XCD-aware blocks, the 234 GB G29 + 100 x key21 footprint, one-deep LDS
+# streaming), no arithmetic: 0.69 ms for 1M x 21 x 64 B (tools/gather_comb.hip,
+# profiles/r03_gather_comb.txt).  The comb moves the same bytes in ~1.04 ms:
+# it is NOT gather-bound (round 2's 1.2 TB/s figure came from uniform gathers
+# over a 64 GiB table without key order and was withdrawn).
+GATHER_ONLY_TBPS = 2.04
 
 
 def table_points(gb: int, qb: int) -> int:
@@ -685,6 +696,19 @@ def main():
     sync_all()
     d.barrier()
     elapsed = time.perf_counter() - t0
+    # the same K steps queued on the context stream only (no overlap between
+    # consecutive batches), reported beside the headline
+    one_stream_ms = None
+    if args.streams and not args.no_extras:
+        d.barrier()
+        sync_all()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            if n:
+                ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, dbs[0].ptr)
+        sync_all()
+        d.barrier()
+        one_stream_ms = d.max(time.perf_counter() - t1) / args.steps * 1e3
     # kernel durations for the roofline: the same K steps again, with HIP events
     # recorded by the library around each scalar / comb launch on its stream
     # (on ONE stream, so no kernel's event window includes another batch's
@@ -720,6 +744,8 @@ def main():
                    "streams": args.streams},
         "check": "pass" if all_ok else "FAIL",
     }
+    if one_stream_ms is not None:
+        out["ms_per_step_one_stream"] = one_stream_ms
     if rank == 0:
         comb_avg = comb_ms / max(comb_cnt, 1) * 1e-3
         scal_avg = scal_ms / max(scal_cnt, 1) * 1e-3
@@ -744,15 +770,17 @@ def main():
                            "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
                            "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc else None}
         if dom == "ecdsa_comb":
-            # the comb's other bound: random 64-B table gathers (one entry per table point,
-            # ~21 per verify); tools/gather_calib.hip moves the same bytes in the same shape
-            # with no arithmetic at ~1.2 TB/s (profiles/r02_gather_calib.txt)
+            # the comb's table reads (one 64-B entry per table point, ~21 per verify) against
+            # the same reads alone in the comb's pattern (tools/gather_comb.hip: 2.04 TB/s,
+            # profiles/r03_gather_comb.txt): the comb is not gather-bound
             pts = table_points(gb, qb)
             gbytes = n * pts * 64
             out["roofline"]["table_gathers"] = {"bytes_per_launch": gbytes, "points_per_verify": pts,
                                                 "TBps": gbytes / max(comb_avg, 1e-12) / 1e12,
                                                 "gather_only_TBps": GATHER_ONLY_TBPS,
-                                                "source": "tools/gather_calib.hip, profiles/r02_gather_calib.txt"}
+                                                "frac_of_gather_only": gbytes / max(comb_avg, 1e-12) / 1e12 /
+                                                GATHER_ONLY_TBPS,
+                                                "source": "tools/gather_comb.hip, profiles/r03_gather_comb.txt"}
         out["kernels"] = kern
         out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
         out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "what": "pbftv_register_keys: G table + the key tables built on the device (incl. allocation)"}

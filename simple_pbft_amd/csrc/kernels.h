@@ -107,6 +107,33 @@ hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_
 // batches up to this size take the latency path (env PBFTV_WAVE_MAX overrides; 0 disables)
 uint64_t wave_path_max();
 
+// The latency path's mailbox in pinned coherent host memory: a 64-B header,
+// then the inputs of up to cap signatures (hashes cap*32, r||s cap*64, key
+// indices cap*4) and one result byte per signature.  The host writes the
+// inputs, n and then bell = the request's sequence number; an armed kernel
+// (k_ecdsa_wave_armed) waiting for that number serves it; stop = seq cancels
+// the armed kernel, which then reports expired = seq (verify_kernels.h).
+struct QcMail {
+  uint32_t bell, n, stop, expired, cap, pad[11];
+  static constexpr size_t hashes_off() { return 64; }
+  static constexpr size_t sigs_off(uint32_t cap) { return 64 + 32 * (size_t)cap; }
+  static constexpr size_t keys_off(uint32_t cap) { return 64 + 96 * (size_t)cap; }
+  static constexpr size_t res_off(uint32_t cap) { return 64 + 100 * (size_t)cap; }
+  static constexpr size_t bytes(uint32_t cap) { return 64 + 101 * (size_t)cap + 64; }
+};
+struct ArmArgs {
+  QcMail* mail;
+  uint32_t want;       // the request sequence number this launch serves
+  uint64_t budget;     // wall-clock ticks before it gives up
+  uint32_t* dflag;     // device-memory flag (wave 0 -> the other waves)
+  uint32_t waves;      // = the mailbox capacity
+  const uint32_t* key_valid;
+  uint32_t nkeys;
+  const uint32_t* gtab;
+  const uint32_t* const* qtabs;
+};
+hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st);
+
 // ---- SHA-256 (sha256_kernels.hip) ----
 // data must stay readable 4 bytes past every message end (device allocations are padded).
 // order: optional permutation (lane -> message), used for block-count bucketing.

@@ -674,6 +674,19 @@ hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_
   return hipErrorInvalidValue;
 }
 
+bool launch_armed_part_g29(int wg, int wq, const ArmArgs& a, hipStream_t st);
+bool launch_armed_part_g26(int wg, int wq, const ArmArgs& a, hipStream_t st);
+bool launch_armed_part_g24(int wg, int wq, const ArmArgs& a, hipStream_t st);
+bool launch_armed_part_small(int wg, int wq, const ArmArgs& a, hipStream_t st);
+
+hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st) {
+  if (a.waves == 0) return hipErrorInvalidValue;
+  if (launch_armed_part_g29(wg, wq, a, st) || launch_armed_part_g26(wg, wq, a, st) ||
+      launch_armed_part_g24(wg, wq, a, st) || launch_armed_part_small(wg, wq, a, st))
+    return hipGetLastError();
+  return hipErrorInvalidValue;
+}
+
 uint64_t wave_path_max() {
   if (const char* e = getenv("PBFTV_WAVE_MAX")) return strtoull(e, nullptr, 10);
   return 2048;

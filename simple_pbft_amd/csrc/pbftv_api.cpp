@@ -39,6 +39,13 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// inside helpers returning hipError_t
+#define HIP_TRY_E(expr)             \
+  do {                              \
+    hipError_t e2_ = (expr);        \
+    if (e2_ != hipSuccess) return e2_; \
+  } while (0)
+
 #define HIP_TRY(expr)                                                                                         \
   do {                                                                                                        \
     hipError_t e_ = (expr);                                                                                   \
@@ -139,7 +146,13 @@ struct Device {
   // ecdsa scratch
   DevBuf hashes, sigs, key_idx, bitmap;
   VerifyScratch vs;  // the lane path's stage-1 records, prefix products, key order, result bytes
-  HostBuf stage;  // zero-copy inputs/outputs of the small-batch path
+  HostBuf stage;  // zero-copy inputs/outputs of the small-batch path (a QcMail mailbox)
+  // the armed latency kernel (k_ecdsa_wave_armed): launched on qstream after
+  // every latency-path call, it waits for the next request's doorbell in
+  // `stage`; arm_seq = the request number it waits for (0: none armed)
+  hipStream_t qstream = nullptr;
+  DevBuf qflag;
+  uint32_t arm_seq = 0, seq_counter = 0;
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
   static constexpr int kSlots = 16;  // chunks staged ahead at most (PBFTV_HOST_SLOTS, default 16)
@@ -248,6 +261,63 @@ hipError_t collect_times(Device& d) {
     }
     d.pending[k].clear();
   }
+  return hipSuccess;
+}
+
+// ---- the armed latency kernel (verify_kernels.h k_ecdsa_wave_armed) ----
+using pbftv::ArmArgs;
+using pbftv::QcMail;
+constexpr uint32_t kQcCap = 128;  // signatures per latency-path call (mailbox capacity, armed waves)
+
+bool qc_arm_enabled() {
+  const char* e = getenv("PBFTV_QC_ARM");
+  return e ? e[0] == '1' : true;
+}
+
+// wall-clock ticks the armed kernel waits for its request (PBFTV_QC_ARM_MS, default 500 ms)
+uint64_t qc_arm_budget() {
+  static const uint64_t ticks = [] {
+    double ms = 500.0;
+    if (const char* e = getenv("PBFTV_QC_ARM_MS")) ms = atof(e);
+    int khz = 100000;
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    return (uint64_t)(ms * khz);
+  }();
+  return ticks;
+}
+
+QcMail* qc_mail(Device& d) { return d.stage.as<QcMail>(); }
+
+hipError_t qc_mail_ready(Device& d) {
+  if (d.stage.cap >= QcMail::bytes(kQcCap)) return hipSuccess;
+  HIP_TRY_E(d.stage.ensure(QcMail::bytes(kQcCap)));
+  std::memset(d.stage.p, 0, QcMail::bytes(kQcCap));
+  qc_mail(d)->cap = kQcCap;
+  return hipSuccess;
+}
+
+// Cancel the armed kernel (if any) and wait until its waves have exited.
+hipError_t qc_disarm(Device& d) {
+  if (!d.arm_seq) return hipSuccess;
+  __atomic_store_n(&qc_mail(d)->stop, d.arm_seq, __ATOMIC_RELEASE);
+  d.arm_seq = 0;
+  return hipStreamSynchronize(d.qstream);
+}
+
+// Launch the kernel that will serve the next latency-path request.
+hipError_t qc_arm(Device& d) {
+  if (d.arm_seq || !qc_arm_enabled() || !d.have_keys) return hipSuccess;
+  HIP_TRY_E(qc_mail_ready(d));
+  if (!d.qstream) HIP_TRY_E(hipStreamCreateWithFlags(&d.qstream, hipStreamNonBlocking));
+  if (!d.qflag.p) {
+    HIP_TRY_E(d.qflag.ensure(64));
+    HIP_TRY_E(hipMemset(d.qflag.p, 0, 64));
+  }
+  const uint32_t want = ++d.seq_counter;
+  const ArmArgs a{qc_mail(d), want, qc_arm_budget(), d.qflag.as<uint32_t>(), kQcCap, d.key_valid.as<uint32_t>(),
+                  d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>()};
+  HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream));
+  d.arm_seq = want;
   return hipSuccess;
 }
 
@@ -522,6 +592,9 @@ void pbftv_close(pbftv_ctx* ctx) {
   for (auto& d : ctx->devs) {
     std::lock_guard<std::mutex> lk(d->mu);
     (void)hipSetDevice(d->id);
+    (void)qc_disarm(*d);  // the armed latency kernel exits before anything is freed
+    if (d->qstream) (void)hipStreamDestroy(d->qstream);
+    d->qflag.release();
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
     for (auto& b : d->qblocks) b->release();
@@ -934,6 +1007,7 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
     auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(qc_disarm(d));  // the armed latency kernel reads the tables too (and would hold the sync)
     d.have_keys = false;
     // every stream of the GPU, not only ours: a verify enqueued on a caller
     // stream (pbftv_stream_create + *_dev) may still read the tables, key_valid
@@ -1012,6 +1086,7 @@ int pbftv_add_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* o
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(qc_disarm(d));
     HIP_TRY(hipDeviceSynchronize());  // caller streams too: qptrs and key_valid are rewritten
     return build_key_tables(d, le, d.nkeys, k, first ? valid.data() : nullptr);
   });
@@ -1039,6 +1114,7 @@ int pbftv_set_key(pbftv_ctx* ctx, uint32_t index, const uint8_t* pub_xy, uint8_t
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(qc_disarm(d));
     HIP_TRY(hipDeviceSynchronize());  // no verify on any stream (caller streams too) still reads the old table
     return build_key_tables(d, le, index, 1, first ? &valid : nullptr);
   });
@@ -1228,31 +1304,76 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
   if (n && n <= pbftv::wave_path_max()) {
     // latency path on the first device: inputs packed into pinned coherent
-    // host memory that the kernel reads directly, one byte per signature
-    // written back the same way and polled for (sentinel 0xFF) -- one launch,
-    // no copies, no stream synchronisation on the fast path.
+    // host memory (the QcMail mailbox) that the kernel reads directly, one byte
+    // per signature written back the same way and polled for (sentinel 0xFF):
+    // no copies, no stream synchronisation on the fast path.  Up to kQcCap
+    // signatures are served by the ARMED kernel launched at the end of the
+    // previous call (k_ecdsa_wave_armed: the request rings its doorbell, no
+    // launch on the critical path); otherwise, or when it expired, one launch of
+    // k_ecdsa_wave.  The next armed kernel is launched while this request
+    // computes (it queues behind the current one on qstream).
     Device& d = *ctx->devs[0];
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    const size_t oh = 0, os = 32 * n, ok = 96 * n, oo = 100 * n;
-    HIP_TRY(d.stage.ensure(oo + n + 64));
+    const bool small = n <= kQcCap;
+    if (!small) HIP_TRY(qc_disarm(d));  // (the mailbox is relaid out for n)
+    const uint32_t cap = small ? kQcCap : (uint32_t)n;
+    if (d.stage.cap < QcMail::bytes(cap)) {
+      HIP_TRY(qc_disarm(d));
+      HIP_TRY(d.stage.ensure(QcMail::bytes(cap)));
+      std::memset(d.stage.p, 0, QcMail::bytes(cap));
+    }
+    QcMail* m = qc_mail(d);
     uint8_t* st8 = d.stage.as<uint8_t>();
-    std::memcpy(st8 + oh, hashes, 32 * n);
-    std::memcpy(st8 + os, sig_rs, 64 * n);
-    std::memcpy(st8 + ok, key_idx, 4 * n);
-    std::memset(st8 + oo, 0xFF, n);
-    HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
-      return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, st8 + oh, st8 + os, reinterpret_cast<uint32_t*>(st8 + ok), n,
-                                      d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
-                                      d.qptrs.as<const uint32_t* const>(), nullptr, st8 + oo, d.stream);
-    }));
+    uint8_t* const hp = st8 + QcMail::hashes_off();
+    uint8_t* const sp = st8 + QcMail::sigs_off(cap);
+    uint32_t* const kp = reinterpret_cast<uint32_t*>(st8 + QcMail::keys_off(cap));
+    volatile uint8_t* const res = st8 + QcMail::res_off(cap);
+    std::memcpy(hp, hashes, 32 * n);
+    std::memcpy(sp, sig_rs, 64 * n);
+    std::memcpy(kp, key_idx, 4 * n);
+    std::memset(const_cast<uint8_t*>(res), 0xFF, n);
+    m->cap = cap;
+    m->n = (uint32_t)n;
+    auto launch_plain = [&]() -> int {
+      HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
+        return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n, d.key_valid.as<uint32_t>(), d.nkeys,
+                                        d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,
+                                        const_cast<uint8_t*>(res), d.stream);
+      }));
+      return PBFTV_OK;
+    };
+    uint32_t cur = 0;  // the armed request number serving this call
+    if (small && d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) != d.arm_seq) {
+      cur = d.arm_seq;
+      d.arm_seq = 0;
+      __atomic_store_n(&m->bell, cur, __ATOMIC_RELEASE);  // inputs and n are in: ring
+    } else {
+      HIP_TRY(qc_disarm(d));
+      int rc = launch_plain();
+      if (rc != PBFTV_OK) return rc;
+    }
+    if (small) HIP_TRY(qc_arm(d));  // the next call's kernel, queued behind this one
     // every wave writes its byte after its last read of the inputs, so once
-    // all n bytes are in, the staging area is free for the next call
-    const volatile uint8_t* res = st8 + oo;
-    const auto t0 = std::chrono::steady_clock::now();
+    // all n bytes are in, the mailbox is free for the next call
+    auto t0 = std::chrono::steady_clock::now();
     for (uint64_t next = 0; next < n;) {
       if (res[next] != 0xFF) {
         ++next;
+        continue;
+      }
+      if (cur && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == cur) {
+        // the armed kernel gave up (budget or cancel) before it saw the bell:
+        // cancel its successor, wait for both to leave, then launch
+        HIP_TRY(qc_disarm(d));
+        HIP_TRY(hipStreamSynchronize(d.qstream));
+        cur = 0;
+        std::memset(const_cast<uint8_t*>(res), 0xFF, n);
+        int rc = launch_plain();
+        if (rc != PBFTV_OK) return rc;
+        HIP_TRY(qc_arm(d));
+        next = 0;
+        t0 = std::chrono::steady_clock::now();
         continue;
       }
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {

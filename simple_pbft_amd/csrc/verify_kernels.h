@@ -995,18 +995,16 @@ __device__ __forceinline__ bool wave_check(const xyzz_s& P, bool finite, const f
   return finite && ((bz & 1ull) != 0 || (rn_ok && (bz & 2ull) != 0));
 }
 
+// Go's verdict for signature i, computed by the whole wave (every lane must
+// call it; wave-uniform result).
 template <int WG, int WQ>
-__global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ hashes,
-                                                   const uint8_t* __restrict__ sigs,
-                                                   const uint32_t* __restrict__ key_idx, uint64_t n,
-                                                   const uint32_t* __restrict__ key_valid, uint32_t nkeys,
-                                                   const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
-                                                   uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+__device__ __forceinline__ bool wave_verify_sig(const uint8_t* __restrict__ hashes, const uint8_t* __restrict__ sigs,
+                                                const uint32_t* __restrict__ key_idx, uint64_t i,
+                                                const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                                const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
   constexpr int nW = nG > nQ ? nG : nQ;
   static_assert(nW <= 64, "one lane per window");
-  const int j = threadIdx.x;
-  const uint64_t i = blockIdx.x;
   bool ok = false;
   uint32_t r[8], s[8], e[8];
   load_be256(hashes + 32 * i, e);  // issued with sig_ok's loads: one round trip to the (host) inputs
@@ -1034,7 +1032,19 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
       ok = ecdsa_check(P, !inf, r);
     }
   }
-  if (j != 0) return;
+  return ok;
+}
+
+template <int WG, int WQ>
+__global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ hashes,
+                                                   const uint8_t* __restrict__ sigs,
+                                                   const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                   const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                                   const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
+                                                   uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+  const uint64_t i = blockIdx.x;
+  const bool ok = wave_verify_sig<WG, WQ>(hashes, sigs, key_idx, i, key_valid, nkeys, gtab, qtabs);
+  if (threadIdx.x != 0) return;
   if (okbytes) {
     okbytes[i] = ok ? 1 : 0;
     return;
@@ -1052,6 +1062,74 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
   if (i + 1 == n) clear |= ((0xFEu << (unsigned)(i & 7)) & 0xFFu) << sh;
   if (clear) atomicAnd(word, ~clear);
   if (ok) atomicOr(word, bit);
+}
+
+// ---- the armed latency kernel ------------------------------------------------
+// Launched AHEAD of the request it serves (pbftv_api.cpp arms one after every
+// latency-path call), so the launch is off the critical path.  Its waves wait
+// on a doorbell in pinned coherent host memory (QcMail, kernels.h): the first
+// kArmPollers waves read the host word themselves; wave 0 also publishes what
+// it saw in a device-memory flag, which the other waves read (one PCIe poller
+// per ~request instead of one per wave).  Every wave reaches an exit: the
+// request (bell == want), a cancel (stop == want), or the budget (wave 0
+// gives up after `budget` wall-clock ticks and tells the others through the
+// flag; a wave that hears nothing gives up after twice that).  On a cancel or
+// expiry wave 0 writes expired = want, and the host serves the request with a
+// fresh launch instead.  Waves with an index >= n exit without work.  The
+// waits use s_sleep between reads; all loads of host words are system-scope
+// atomics (no stale cache line), and nothing is written through the scalar
+// cache.
+constexpr int kArmPollers = 8;
+
+template <int WG, int WQ>
+__global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ mail, uint32_t want, uint64_t budget,
+                                                         uint32_t* __restrict__ dflag,
+                                                         const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                                         const uint4* __restrict__ gtab,
+                                                         const uint4* const* __restrict__ qtabs) {
+  const uint32_t b = blockIdx.x;
+  const uint64_t t0 = wall_clock64();
+  const uint32_t go = 2 * want, quit = 2 * want + 1;  // device-flag values for this arming
+  bool serve = false;
+  for (;;) {
+    if (b < (uint32_t)kArmPollers) {
+      if (__hip_atomic_load(&mail->bell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == want) {
+        serve = true;
+        break;
+      }
+    }
+    const uint32_t f = __hip_atomic_load(dflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (f == go) {
+      serve = true;
+      break;
+    }
+    if (f == quit) break;
+    const uint64_t dt = wall_clock64() - t0;
+    if (b == 0 && (dt > budget || __hip_atomic_load(&mail->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == want))
+      break;
+    if (dt > 2 * budget) break;  // never heard from wave 0: give up too
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (b == 0 && threadIdx.x == 0) {
+    __hip_atomic_store(dflag, serve ? go : quit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (!serve) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (!serve) return;
+  const uint32_t n = __hip_atomic_load(&mail->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (b >= n) return;
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(mail);
+  const uint32_t cap = mail->cap;
+  const bool ok = wave_verify_sig<WG, WQ>(base + QcMail::hashes_off(), base + QcMail::sigs_off(cap),
+                                          reinterpret_cast<const uint32_t*>(base + QcMail::keys_off(cap)), b,
+                                          key_valid, nkeys, gtab, qtabs);
+  if (threadIdx.x == 0) reinterpret_cast<volatile uint8_t*>(mail)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
+}
+
+template <int WG, int WQ>
+void launch_armed_w(const ArmArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3(a.waves), dim3(64), 0, st, a.mail, a.want, a.budget, a.dflag,
+                     a.key_valid, a.nkeys, reinterpret_cast<const uint4*>(a.gtab),
+                     reinterpret_cast<const uint4* const*>(a.qtabs));
 }
 
 template <int WG, int WQ>
@@ -1082,10 +1160,19 @@ void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint
   bool launch_wave_part_##NAME(int wg, int wq, const WaveArgs& a, hipStream_t st) {                           \
     COMBOS(PBFTV_PART_WAVE_CASE)                                                                              \
     return false;                                                                                             \
+  }                                                                                                           \
+  bool launch_armed_part_##NAME(int wg, int wq, const ArmArgs& a, hipStream_t st) {                           \
+    COMBOS(PBFTV_PART_ARMED_CASE)                                                                             \
+    return false;                                                                                             \
   }
 #define PBFTV_PART_COMB_CASE(G, Q)                                                                            \
   if (wg == G && wq == Q) {                                                                                   \
     launch_comb_w<G, Q>(a.rec, a.n, a.gtab, a.qtabs, a.bitmap, a.okb, st);                                    \
+    return true;                                                                                              \
+  }
+#define PBFTV_PART_ARMED_CASE(G, Q)                                                                           \
+  if (wg == G && wq == Q) {                                                                                   \
+    launch_armed_w<G, Q>(a, st);                                                                              \
     return true;                                                                                              \
   }
 #define PBFTV_PART_WAVE_CASE(G, Q)                                                                            \

@@ -398,3 +398,40 @@ def test_dev_calls_on_two_streams_share_scratch(ver, oracle_lib, monkeypatch):
         for tup in bufs:
             for b in tup:
                 b.free()
+
+
+# ---- the armed latency kernel (pbftv_api.cpp qc_arm / k_ecdsa_wave_armed) ----
+@pytest.mark.parametrize("arm_ms", ["500", "1"])
+def test_armed_latency_path(oracle_lib, arm_ms, monkeypatch):
+    """Small host-buffer batches are served by the kernel armed at the end of
+    the previous call (doorbell in host memory).  Consecutive calls of every
+    size up to the mailbox capacity and past it, a key change while armed,
+    and -- with a 1 ms budget and pauses -- the armed kernel expiring so the
+    request falls back to a fresh launch; every bitmap against the oracle."""
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", arm_ms)
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=5, per_key=60, seed=77)
+    sigs[::7, 45] ^= 0x20
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    rng = np.random.default_rng(78)
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        for it, n in enumerate([1, 3, 3, 67, 128, 129, 300, 2, 64, 5, 127, 1, 3]):
+            o = rng.choice(n_all, n, replace=False)
+            got = v.verify_batch(hashes[o], sigs[o], kidx[o])
+            assert (got == want[o]).all(), (it, n)
+            if arm_ms == "1" and it % 3 == 1:
+                time.sleep(0.01)  # let the armed kernel expire
+        # a key change while a kernel is armed: it is cancelled first
+        assert v.set_key(0, keys[0])
+        o = rng.choice(n_all, 3, replace=False)
+        assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all()
+        for _ in range(200):  # back to back, the quorum count too
+            o = rng.choice(n_all, 3, replace=False)
+            bm, acc, ok = v.qc_verify(hashes[o], sigs[o], kidx[o], quorum=3)
+            assert (bm == want[o]).all() and acc == int(want[o].sum()) and ok == bool(want[o].all())

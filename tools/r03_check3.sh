@@ -11,3 +11,5 @@ timeout -k 10 300 python -u tools/qc_fresh.py 4000 > "$OUT/qc_default.json" || e
 cat "$OUT/qc_default.json"
 PBFTV_GBITS=24 timeout -k 10 300 python -u tools/qc_fresh.py 4000 > "$OUT/qc_g24.json" || exit 1
 cat "$OUT/qc_g24.json"
+timeout -k 10 120 ./tools/launch_rt 5000 > "$OUT/launch_rt.json" || exit 1
+cat "$OUT/launch_rt.json"
