@@ -113,13 +113,20 @@ uint64_t wave_path_max();
 // inputs, n and then bell = the request's sequence number; an armed kernel
 // (k_ecdsa_wave_armed) waiting for that number serves it; stop = seq cancels
 // the armed kernel, which then reports expired = seq (verify_kernels.h).
+// The first kQcSlots signatures are also written to their own 3-line slot
+// (slot_off): line 0 = {tag, n, key, 0, hash[32], 0, 0, 0, tag}, line 1 =
+// {tag, 0, 0, 0, r[32], 0, 0, 0, tag}, line 2 likewise with s; the tags (the
+// request number) are written after their line's data, the last dword first.
 struct QcMail {
   uint32_t bell, n, stop, expired, cap, pad[11];
-  static constexpr size_t hashes_off() { return 64; }
-  static constexpr size_t sigs_off(uint32_t cap) { return 64 + 32 * (size_t)cap; }
-  static constexpr size_t keys_off(uint32_t cap) { return 64 + 96 * (size_t)cap; }
-  static constexpr size_t res_off(uint32_t cap) { return 64 + 100 * (size_t)cap; }
-  static constexpr size_t bytes(uint32_t cap) { return 64 + 101 * (size_t)cap + 64; }
+  static constexpr uint32_t kQcSlots = 8;
+  static constexpr size_t slot_off(uint32_t i) { return 64 + 192 * (size_t)i; }
+  static constexpr size_t arrays_off() { return 64 + 192 * (size_t)kQcSlots; }
+  static constexpr size_t hashes_off() { return arrays_off(); }
+  static constexpr size_t sigs_off(uint32_t cap) { return arrays_off() + 32 * (size_t)cap; }
+  static constexpr size_t keys_off(uint32_t cap) { return arrays_off() + 96 * (size_t)cap; }
+  static constexpr size_t res_off(uint32_t cap) { return arrays_off() + 100 * (size_t)cap; }
+  static constexpr size_t bytes(uint32_t cap) { return arrays_off() + 101 * (size_t)cap + 64; }
 };
 struct ArmArgs {
   QcMail* mail;

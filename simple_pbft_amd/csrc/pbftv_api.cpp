@@ -1347,6 +1347,24 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     if (small && d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) != d.arm_seq) {
       cur = d.arm_seq;
       d.arm_seq = 0;
+      // the first signatures' slots: each line's data, then its tag (a line is
+      // read by the GPU as one snapshot, and x86 stores become visible in order)
+      for (uint32_t i = 0; i < QcMail::kQcSlots; ++i) {
+        uint32_t* l0 = reinterpret_cast<uint32_t*>(st8 + QcMail::slot_off(i));
+        uint32_t* l1 = l0 + 16;
+        uint32_t* l2 = l0 + 32;
+        if (i < n) {
+          std::memcpy(l0 + 4, hashes + 32 * i, 32);
+          std::memcpy(l1 + 4, sig_rs + 64 * i, 32);
+          std::memcpy(l2 + 4, sig_rs + 64 * i + 32, 32);
+          l0[2] = key_idx[i];
+        }
+        l0[1] = (uint32_t)n;
+        for (uint32_t* l : {l1, l2, l0}) {
+          __atomic_store_n(l + 15, cur, __ATOMIC_RELEASE);
+          __atomic_store_n(l, cur, __ATOMIC_RELEASE);
+        }
+      }
       __atomic_store_n(&m->bell, cur, __ATOMIC_RELEASE);  // inputs and n are in: ring
     } else {
       HIP_TRY(qc_disarm(d));

@@ -995,44 +995,54 @@ __device__ __forceinline__ bool wave_check(const xyzz_s& P, bool finite, const f
   return finite && ((bz & 1ull) != 0 || (rn_ok && (bz & 2ull) != 0));
 }
 
-// Go's verdict for signature i, computed by the whole wave (every lane must
-// call it; wave-uniform result).
+// Go's verdict from uniform LE words e (hash), r, s, the key's table and
+// whether the key is registered and valid, computed by the whole wave (every
+// lane must call it; wave-uniform result).
+template <int WG, int WQ>
+__device__ __forceinline__ bool wave_verify_words(uint32_t e[8], uint32_t r[8], uint32_t s[8], bool key_ok,
+                                                  const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
+  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  constexpr int nW = nG > nQ ? nG : nQ;
+  static_assert(nW <= 64, "one lane per window");
+  if (!key_ok || words_is_zero(r) || words_is_zero(s) || !words_lt(r, kN32) || !words_lt(s, kN32)) return false;
+  uint32_t u1[8], u2[8];
+  fe rm, rnm;
+  bool rn_ok;
+  wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
+  bool inf, ok = false;
+  bool exc = true;
+  if constexpr (nW > 8 && nW <= 16) {
+    const bool okq = wave_verify_quads<WG, WQ>(exc, u1, u2, gtab, qtab, rm, rnm, rn_ok);
+    exc = __any(exc);
+    ok = __builtin_amdgcn_readfirstlane((int)okq) != 0;  // lane 0 = quad 0: the all-reduced verdict
+  }
+  if (exc) {  // windows outnumber the quads, or a doubling somewhere: exact lane-per-window rerun
+    jac P;
+    wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qtab);
+    ok = ecdsa_check(P, !inf, r);
+  }
+  return ok;
+}
+
+// ... from memory: signature i of the (host or device) input arrays.
 template <int WG, int WQ>
 __device__ __forceinline__ bool wave_verify_sig(const uint8_t* __restrict__ hashes, const uint8_t* __restrict__ sigs,
                                                 const uint32_t* __restrict__ key_idx, uint64_t i,
                                                 const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                 const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs) {
-  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
-  constexpr int nW = nG > nQ ? nG : nQ;
-  static_assert(nW <= 64, "one lane per window");
-  bool ok = false;
   uint32_t r[8], s[8], e[8];
-  load_be256(hashes + 32 * i, e);  // issued with sig_ok's loads: one round trip to the (host) inputs
-  if (sig_ok(sigs, key_idx, key_valid, nkeys, i, r, s)) {  // wave-uniform branch
-    PBFTV_UNROLL for (int k = 0; k < 8; ++k) {  // one copy per wave (the loads are per lane)
-      e[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[k]);
-      r[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[k]);
-      s[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[k]);
-    }
-    const uint4* qtab = qtabs[key_idx[i]];  // (loaded now: ready when the scalars are)
-    uint32_t u1[8], u2[8];
-    fe rm, rnm;
-    bool rn_ok;
-    wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
-    bool inf;
-    bool exc = true;
-    if constexpr (nW > 8 && nW <= 16) {
-      const bool okq = wave_verify_quads<WG, WQ>(exc, u1, u2, gtab, qtab, rm, rnm, rn_ok);
-      exc = __any(exc);
-      ok = __builtin_amdgcn_readfirstlane((int)okq) != 0;  // lane 0 = quad 0: the all-reduced verdict
-    }
-    if (exc) {  // windows outnumber the quads, or a doubling somewhere: exact lane-per-window rerun
-      jac P;
-      wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qtab);
-      ok = ecdsa_check(P, !inf, r);
-    }
+  load_be256(hashes + 32 * i, e);  // one round trip to the (host) inputs
+  load_be256(sigs + 64 * i, r);
+  load_be256(sigs + 64 * i + 32, s);
+  const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)key_idx[i]);
+  const bool key_ok = k < nkeys && key_valid[k] != 0;
+  const uint4* qtab = qtabs[k < nkeys ? k : 0];  // (loaded now: ready when the scalars are)
+  PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // one copy per wave (the loads are per lane)
+    e[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[t]);
+    r[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[t]);
+    s[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[t]);
   }
-  return ok;
+  return wave_verify_words<WG, WQ>(e, r, s, key_ok, gtab, qtab);
 }
 
 template <int WG, int WQ>
@@ -1079,6 +1089,15 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
 // waits use s_sleep between reads; all loads of host words are system-scope
 // atomics (no stale cache line), and nothing is written through the scalar
 // cache.
+// The first kArmPollers signatures of a request also travel in their own
+// slot (QcMail::slot_off): three 64-B lines, each tagged with the request
+// number in its first and last dword, holding n, the key and the hash / r / s.  Those waves poll their
+// three lines in one wave-wide load (lane l reads dword l % 16 of line l / 16):
+// a line is one cache line of the host, read as one snapshot, and the host
+// writes each tag after the data of its line, so three matching tags mean the
+// whole input is in registers -- no second PCIe round trip after the bell.
+// Every wave also loads the table pointers and validity flags of the first
+// 128 keys while it waits.
 constexpr int kArmPollers = 8;
 
 template <int WG, int WQ>
@@ -1087,14 +1106,28 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
                                                          const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                          const uint4* __restrict__ gtab,
                                                          const uint4* const* __restrict__ qtabs) {
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = blockIdx.x, lane = threadIdx.x;
   const uint64_t t0 = wall_clock64();
   const uint32_t go = 2 * want, quit = 2 * want + 1;  // device-flag values for this arming
-  bool serve = false;
+  // key data for keys < 128, two per lane (lane l: keys l and l + 64)
+  const uint4* qt_lo = lane < nkeys ? qtabs[lane] : nullptr;
+  const uint4* qt_hi = lane + 64 < nkeys ? qtabs[lane + 64] : nullptr;
+  const uint32_t kv_lo = lane < nkeys ? key_valid[lane] : 0u, kv_hi = lane + 64 < nkeys ? key_valid[lane + 64] : 0u;
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(mail);
+  const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b < kArmPollers ? b : 0));
+  uint32_t v = 0;
+  bool serve = false, have = false;
   for (;;) {
     if (b < (uint32_t)kArmPollers) {
-      if (__hip_atomic_load(&mail->bell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == want) {
-        serve = true;
+      v = __hip_atomic_load(slot + (lane & 15) + 16 * (lane >> 4 < 3 ? lane >> 4 : 2), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_SYSTEM);
+      // head AND tail tag of every line: even a read that tore a line in two
+      // would show the data of both halves new once both tags are
+      const bool tags = __builtin_amdgcn_readlane(v, 0) == want && __builtin_amdgcn_readlane(v, 15) == want &&
+                        __builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
+                        __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want;
+      if (tags) {
+        serve = have = true;
         break;
       }
     }
@@ -1110,19 +1143,49 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
     if (dt > 2 * budget) break;  // never heard from wave 0: give up too
     __builtin_amdgcn_s_sleep(1);
   }
-  if (b == 0 && threadIdx.x == 0) {
+  if (b == 0 && lane == 0) {
     __hip_atomic_store(dflag, serve ? go : quit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (!serve) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (!serve) return;
-  const uint32_t n = __hip_atomic_load(&mail->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint32_t n = have ? __builtin_amdgcn_readlane(v, 1)
+                          : __hip_atomic_load(&mail->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (b >= n) return;
-  const uint8_t* base = reinterpret_cast<const uint8_t*>(mail);
-  const uint32_t cap = mail->cap;
-  const bool ok = wave_verify_sig<WG, WQ>(base + QcMail::hashes_off(), base + QcMail::sigs_off(cap),
-                                          reinterpret_cast<const uint32_t*>(base + QcMail::keys_off(cap)), b,
-                                          key_valid, nkeys, gtab, qtabs);
-  if (threadIdx.x == 0) reinterpret_cast<volatile uint8_t*>(mail)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
+  uint32_t e[8], r[8], s[8], k;
+  if (have) {  // slot line j dword 4 + t = LE dword t of the hash / r / s
+    k = __builtin_amdgcn_readlane(v, 2);
+    PBFTV_UNROLL for (int t = 0; t < 8; ++t) {
+      e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 4 + t));
+      r[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 20 + t));
+      s[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 36 + t));
+    }
+  } else {
+    const uint32_t cap = mail->cap;
+    load_be256(base + QcMail::hashes_off() + 32 * b, e);
+    load_be256(base + QcMail::sigs_off(cap) + 64 * b, r);
+    load_be256(base + QcMail::sigs_off(cap) + 64 * b + 32, s);
+    k = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)reinterpret_cast<const uint32_t*>(base + QcMail::keys_off(cap))[b]);
+    PBFTV_UNROLL for (int t = 0; t < 8; ++t) {
+      e[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[t]);
+      r[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[t]);
+      s[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[t]);
+    }
+  }
+  bool key_ok;
+  const uint4* qtab;
+  if (k < 128 && k < nkeys) {  // prefetched
+    const int kl = (int)(k & 63);
+    const uint64_t ql = (uint64_t)(uintptr_t)(k < 64 ? qt_lo : qt_hi);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ql, kl), hi = __builtin_amdgcn_readlane((uint32_t)(ql >> 32), kl);
+    qtab = reinterpret_cast<const uint4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+    key_ok = __builtin_amdgcn_readlane(k < 64 ? kv_lo : kv_hi, kl) != 0;
+  } else {
+    key_ok = k < nkeys && key_valid[k] != 0;
+    qtab = qtabs[k < nkeys ? k : 0];
+  }
+  const bool ok = wave_verify_words<WG, WQ>(e, r, s, key_ok, gtab, qtab);
+  if (lane == 0) reinterpret_cast<volatile uint8_t*>(mail)[QcMail::res_off(mail->cap) + b] = ok ? 1 : 0;
 }
 
 template <int WG, int WQ>
