@@ -147,11 +147,11 @@ struct Device {
   DevBuf hashes, sigs, key_idx, bitmap;
   VerifyScratch vs;  // the lane path's stage-1 records, prefix products, key order, result bytes
   HostBuf stage;  // zero-copy inputs/outputs of the small-batch path (a QcMail mailbox)
-  // the armed latency kernel (k_ecdsa_wave_armed): launched on qstream after
-  // every latency-path call, it waits for the next request's doorbell in
-  // `stage`; arm_seq = the request number it waits for (0: none armed)
-  hipStream_t qstream = nullptr;
-  DevBuf qflag;
+  // the armed latency kernel (k_ecdsa_wave_armed): launched after every
+  // latency-path call, it waits for the next request's doorbell in `stage`;
+  // arm_seq = the request number it waits for (0: none armed)
+  hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: the next kernel spins while this one works
+  DevBuf qflag;                                 // per stream slot: {go/quit flag, n} in its own 64 B
   uint32_t arm_seq = 0, seq_counter = 0;
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
@@ -296,27 +296,29 @@ hipError_t qc_mail_ready(Device& d) {
   return hipSuccess;
 }
 
-// Cancel the armed kernel (if any) and wait until its waves have exited.
+// Cancel the armed kernel (if any) and wait until every armed kernel has exited.
 hipError_t qc_disarm(Device& d) {
-  if (!d.arm_seq) return hipSuccess;
-  __atomic_store_n(&qc_mail(d)->stop, d.arm_seq, __ATOMIC_RELEASE);
+  if (d.arm_seq) __atomic_store_n(&qc_mail(d)->stop, d.arm_seq, __ATOMIC_RELEASE);
   d.arm_seq = 0;
-  return hipStreamSynchronize(d.qstream);
+  for (hipStream_t q : d.qstream)
+    if (q) HIP_TRY_E(hipStreamSynchronize(q));
+  return hipSuccess;
 }
 
 // Launch the kernel that will serve the next latency-path request.
 hipError_t qc_arm(Device& d) {
   if (d.arm_seq || !qc_arm_enabled() || !d.have_keys) return hipSuccess;
   HIP_TRY_E(qc_mail_ready(d));
-  if (!d.qstream) HIP_TRY_E(hipStreamCreateWithFlags(&d.qstream, hipStreamNonBlocking));
+  for (hipStream_t& q : d.qstream)
+    if (!q) HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
   if (!d.qflag.p) {
-    HIP_TRY_E(d.qflag.ensure(64));
-    HIP_TRY_E(hipMemset(d.qflag.p, 0, 64));
+    HIP_TRY_E(d.qflag.ensure(128));
+    HIP_TRY_E(hipMemset(d.qflag.p, 0, 128));
   }
-  const uint32_t want = ++d.seq_counter;
-  const ArmArgs a{qc_mail(d), want, qc_arm_budget(), d.qflag.as<uint32_t>(), kQcCap, d.key_valid.as<uint32_t>(),
-                  d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>()};
-  HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream));
+  const uint32_t want = ++d.seq_counter, slot = want & 1u;
+  const ArmArgs a{qc_mail(d), want, qc_arm_budget(), d.qflag.as<uint32_t>() + 16 * slot, kQcCap,
+                  d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>()};
+  HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = want;
   return hipSuccess;
 }
@@ -592,8 +594,9 @@ void pbftv_close(pbftv_ctx* ctx) {
   for (auto& d : ctx->devs) {
     std::lock_guard<std::mutex> lk(d->mu);
     (void)hipSetDevice(d->id);
-    (void)qc_disarm(*d);  // the armed latency kernel exits before anything is freed
-    if (d->qstream) (void)hipStreamDestroy(d->qstream);
+    (void)qc_disarm(*d);  // the armed latency kernels exit before anything is freed
+    for (hipStream_t q : d->qstream)
+      if (q) (void)hipStreamDestroy(q);
     d->qflag.release();
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
@@ -1311,7 +1314,8 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     // previous call (k_ecdsa_wave_armed: the request rings its doorbell, no
     // launch on the critical path); otherwise, or when it expired, one launch of
     // k_ecdsa_wave.  The next armed kernel is launched while this request
-    // computes (it queues behind the current one on qstream).
+    // computes, on the other of two streams, so it is already spinning when a
+    // back-to-back request rings.
     Device& d = *ctx->devs[0];
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
@@ -1383,8 +1387,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       if (cur && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == cur) {
         // the armed kernel gave up (budget or cancel) before it saw the bell:
         // cancel its successor, wait for both to leave, then launch
-        HIP_TRY(qc_disarm(d));
-        HIP_TRY(hipStreamSynchronize(d.qstream));
+        HIP_TRY(qc_disarm(d));  // (waits for both armed kernels to leave)
         cur = 0;
         std::memset(const_cast<uint8_t*>(res), 0xFF, n);
         int rc = launch_plain();

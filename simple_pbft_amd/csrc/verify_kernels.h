@@ -1143,13 +1143,17 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
     if (dt > 2 * budget) break;  // never heard from wave 0: give up too
     __builtin_amdgcn_s_sleep(1);
   }
+  // wave 0 learns n with its slot (it always serves signature 0) and hands it
+  // to the other waves with the go flag (dflag[1], then dflag[0]: device
+  // memory, no second trip over PCIe)
+  uint32_t n = have ? __builtin_amdgcn_readlane(v, 1) : 0u;
   if (b == 0 && lane == 0) {
+    if (serve) __hip_atomic_store(dflag + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(dflag, serve ? go : quit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (!serve) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (!serve) return;
-  const uint32_t n = have ? __builtin_amdgcn_readlane(v, 1)
-                          : __hip_atomic_load(&mail->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!have) n = __hip_atomic_load(dflag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (b >= n) return;
   uint32_t e[8], r[8], s[8], k;
   if (have) {  // slot line j dword 4 + t = LE dword t of the hash / r / s
