@@ -132,8 +132,6 @@ struct ArmArgs {
   QcMail* mail;
   uint32_t want;       // the request sequence number this launch serves
   uint64_t budget;     // wall-clock ticks before it gives up
-  uint32_t* dflag;     // device-memory flag (wave 0 -> the other waves)
-  uint32_t waves;      // = the mailbox capacity
   const uint32_t* key_valid;
   uint32_t nkeys;
   const uint32_t* gtab;

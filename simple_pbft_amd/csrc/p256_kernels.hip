@@ -680,7 +680,6 @@ bool launch_armed_part_g24(int wg, int wq, const ArmArgs& a, hipStream_t st);
 bool launch_armed_part_small(int wg, int wq, const ArmArgs& a, hipStream_t st);
 
 hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st) {
-  if (a.waves == 0) return hipErrorInvalidValue;
   if (launch_armed_part_g29(wg, wq, a, st) || launch_armed_part_g26(wg, wq, a, st) ||
       launch_armed_part_g24(wg, wq, a, st) || launch_armed_part_small(wg, wq, a, st))
     return hipGetLastError();

@@ -151,7 +151,6 @@ struct Device {
   // latency-path call, it waits for the next request's doorbell in `stage`;
   // arm_seq = the request number it waits for (0: none armed)
   hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: the next kernel spins while this one works
-  DevBuf qflag;                                 // per stream slot: {go/quit flag, n} in its own 64 B
   uint32_t arm_seq = 0, seq_counter = 0;
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
@@ -311,13 +310,9 @@ hipError_t qc_arm(Device& d) {
   HIP_TRY_E(qc_mail_ready(d));
   for (hipStream_t& q : d.qstream)
     if (!q) HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-  if (!d.qflag.p) {
-    HIP_TRY_E(d.qflag.ensure(128));
-    HIP_TRY_E(hipMemset(d.qflag.p, 0, 128));
-  }
   const uint32_t want = ++d.seq_counter, slot = want & 1u;
-  const ArmArgs a{qc_mail(d), want, qc_arm_budget(), d.qflag.as<uint32_t>() + 16 * slot, kQcCap,
-                  d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>()};
+  const ArmArgs a{qc_mail(d), want, qc_arm_budget(), d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
+                  d.qptrs.as<const uint32_t* const>()};
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = want;
   return hipSuccess;
@@ -597,7 +592,6 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)qc_disarm(*d);  // the armed latency kernels exit before anything is freed
     for (hipStream_t q : d->qstream)
       if (q) (void)hipStreamDestroy(q);
-    d->qflag.release();
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
     for (auto& b : d->qblocks) b->release();
@@ -1348,7 +1342,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       return PBFTV_OK;
     };
     uint32_t cur = 0;  // the armed request number serving this call
-    if (small && d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) != d.arm_seq) {
+    if (n <= QcMail::kQcSlots && d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) != d.arm_seq) {
       cur = d.arm_seq;
       d.arm_seq = 0;
       // the first signatures' slots: each line's data, then its tag (a line is

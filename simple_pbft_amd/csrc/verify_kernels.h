@@ -1075,106 +1075,62 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
 }
 
 // ---- the armed latency kernel ------------------------------------------------
-// Launched AHEAD of the request it serves (pbftv_api.cpp arms one after every
-// latency-path call), so the launch is off the critical path.  Its waves wait
-// on a doorbell in pinned coherent host memory (QcMail, kernels.h): the first
-// kArmPollers waves read the host word themselves; wave 0 also publishes what
-// it saw in a device-memory flag, which the other waves read (one PCIe poller
-// per ~request instead of one per wave).  Every wave reaches an exit: the
-// request (bell == want), a cancel (stop == want), or the budget (wave 0
-// gives up after `budget` wall-clock ticks and tells the others through the
-// flag; a wave that hears nothing gives up after twice that).  On a cancel or
-// expiry wave 0 writes expired = want, and the host serves the request with a
-// fresh launch instead.  Waves with an index >= n exit without work.  The
-// waits use s_sleep between reads; all loads of host words are system-scope
-// atomics (no stale cache line), and nothing is written through the scalar
-// cache.
-// The first kArmPollers signatures of a request also travel in their own
-// slot (QcMail::slot_off): three 64-B lines, each tagged with the request
-// number in its first and last dword, holding n, the key and the hash / r / s.  Those waves poll their
-// three lines in one wave-wide load (lane l reads dword l % 16 of line l / 16):
-// a line is one cache line of the host, read as one snapshot, and the host
-// writes each tag after the data of its line, so three matching tags mean the
-// whole input is in registers -- no second PCIe round trip after the bell.
-// Every wave also loads the table pointers and validity flags of the first
-// 128 keys while it waits.
-constexpr int kArmPollers = 8;
-
+// Launched AHEAD of the request it serves (pbftv_api.cpp arms one while the
+// previous request computes), so no launch is on the critical path.  One wave
+// per signature slot (QcMail::kQcSlots = 8: a certificate of n = 3f+1 <= 9
+// replicas).  Each wave polls, in ONE wave-wide load (lane l reads dword
+// l % 16 of line l / 16), the three 64-B lines of its slot and the mailbox
+// header: every slot line carries the request number in its first and last
+// dword, written by the host after the line's data (one line is read as one
+// snapshot of the host's cache line, and x86 stores become visible in order;
+// requiring both tags also covers a read that tore a line in two), so three
+// matching lines mean n, the key and the hash / r / s are already in
+// registers -- no second PCIe round trip.  Every wave reaches an exit: its
+// request (tags == want), a cancel (header stop == want) or the budget
+// (wall-clock ticks); a wave that leaves without serving writes
+// expired = want and the host serves the request with a launch instead.
+// Waits are s_sleep between polls; host words are read with system-scope
+// loads; nothing is written through the scalar cache.  The key tables'
+// pointers and validity flags of the first 128 keys are loaded while waiting.
 template <int WG, int WQ>
 __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ mail, uint32_t want, uint64_t budget,
-                                                         uint32_t* __restrict__ dflag,
                                                          const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                          const uint4* __restrict__ gtab,
                                                          const uint4* const* __restrict__ qtabs) {
   const uint32_t b = blockIdx.x, lane = threadIdx.x;
   const uint64_t t0 = wall_clock64();
-  const uint32_t go = 2 * want, quit = 2 * want + 1;  // device-flag values for this arming
   // key data for keys < 128, two per lane (lane l: keys l and l + 64)
   const uint4* qt_lo = lane < nkeys ? qtabs[lane] : nullptr;
   const uint4* qt_hi = lane + 64 < nkeys ? qtabs[lane + 64] : nullptr;
   const uint32_t kv_lo = lane < nkeys ? key_valid[lane] : 0u, kv_hi = lane + 64 < nkeys ? key_valid[lane + 64] : 0u;
   const uint8_t* base = reinterpret_cast<const uint8_t*>(mail);
-  const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b < kArmPollers ? b : 0));
+  const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b));
+  const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
   uint32_t v = 0;
-  bool serve = false, have = false;
+  bool serve = false;
   for (;;) {
-    if (b < (uint32_t)kArmPollers) {
-      v = __hip_atomic_load(slot + (lane & 15) + 16 * (lane >> 4 < 3 ? lane >> 4 : 2), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_SYSTEM);
-      // head AND tail tag of every line: even a read that tore a line in two
-      // would show the data of both halves new once both tags are
-      const bool tags = __builtin_amdgcn_readlane(v, 0) == want && __builtin_amdgcn_readlane(v, 15) == want &&
-                        __builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
-                        __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want;
-      if (tags) {
-        serve = have = true;
-        break;
-      }
-    }
-    const uint32_t f = __hip_atomic_load(dflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (f == go) {
+    v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__builtin_amdgcn_readlane(v, 0) == want && __builtin_amdgcn_readlane(v, 15) == want &&
+        __builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
+        __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want) {
       serve = true;
       break;
     }
-    if (f == quit) break;
-    const uint64_t dt = wall_clock64() - t0;
-    if (b == 0 && (dt > budget || __hip_atomic_load(&mail->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == want))
-      break;
-    if (dt > 2 * budget) break;  // never heard from wave 0: give up too
-    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_readlane(v, 48 + 2) == want || wall_clock64() - t0 > budget) break;  // header stop
+    __builtin_amdgcn_s_sleep(2);
   }
-  // wave 0 learns n with its slot (it always serves signature 0) and hands it
-  // to the other waves with the go flag (dflag[1], then dflag[0]: device
-  // memory, no second trip over PCIe)
-  uint32_t n = have ? __builtin_amdgcn_readlane(v, 1) : 0u;
-  if (b == 0 && lane == 0) {
-    if (serve) __hip_atomic_store(dflag + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(dflag, serve ? go : quit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    if (!serve) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!serve) {
+    if (lane == 0) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
   }
-  if (!serve) return;
-  if (!have) n = __hip_atomic_load(dflag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n = __builtin_amdgcn_readlane(v, 1);
   if (b >= n) return;
-  uint32_t e[8], r[8], s[8], k;
-  if (have) {  // slot line j dword 4 + t = LE dword t of the hash / r / s
-    k = __builtin_amdgcn_readlane(v, 2);
-    PBFTV_UNROLL for (int t = 0; t < 8; ++t) {
-      e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 4 + t));
-      r[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 20 + t));
-      s[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 36 + t));
-    }
-  } else {
-    const uint32_t cap = mail->cap;
-    load_be256(base + QcMail::hashes_off() + 32 * b, e);
-    load_be256(base + QcMail::sigs_off(cap) + 64 * b, r);
-    load_be256(base + QcMail::sigs_off(cap) + 64 * b + 32, s);
-    k = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)reinterpret_cast<const uint32_t*>(base + QcMail::keys_off(cap))[b]);
-    PBFTV_UNROLL for (int t = 0; t < 8; ++t) {
-      e[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[t]);
-      r[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[t]);
-      s[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[t]);
-    }
+  uint32_t e[8], r[8], s[8];
+  const uint32_t k = __builtin_amdgcn_readlane(v, 2);
+  PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // slot line j, dword 4 + t = LE dword t of the hash / r / s
+    e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 4 + t));
+    r[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 20 + t));
+    s[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 36 + t));
   }
   bool key_ok;
   const uint4* qtab;
@@ -1194,7 +1150,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
 
 template <int WG, int WQ>
 void launch_armed_w(const ArmArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3(a.waves), dim3(64), 0, st, a.mail, a.want, a.budget, a.dflag,
+  hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3(QcMail::kQcSlots), dim3(64), 0, st, a.mail, a.want, a.budget,
                      a.key_valid, a.nkeys, reinterpret_cast<const uint4*>(a.gtab),
                      reinterpret_cast<const uint4* const*>(a.qtabs));
 }
