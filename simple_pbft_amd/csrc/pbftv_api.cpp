@@ -1342,7 +1342,8 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       return PBFTV_OK;
     };
     uint32_t cur = 0;  // the armed request number serving this call
-    if (n <= QcMail::kQcSlots && d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) != d.arm_seq) {
+    const bool armable = n <= QcMail::kQcSlots;
+    if (armable && d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) != d.arm_seq) {
       cur = d.arm_seq;
       d.arm_seq = 0;
       // the first signatures' slots: each line's data, then its tag (a line is
@@ -1365,11 +1366,13 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       }
       __atomic_store_n(&m->bell, cur, __ATOMIC_RELEASE);  // inputs and n are in: ring
     } else {
-      HIP_TRY(qc_disarm(d));
+      // a batch the armed kernel cannot take (n > its slots) leaves it armed
+      // for the next small one; an expired one is collected first
+      if (d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == d.arm_seq) HIP_TRY(qc_disarm(d));
       int rc = launch_plain();
       if (rc != PBFTV_OK) return rc;
     }
-    if (small) HIP_TRY(qc_arm(d));  // the next call's kernel, queued behind this one
+    if (small) HIP_TRY(qc_arm(d));  // the next call's kernel (no-op while one is armed)
     // every wave writes its byte after its last read of the inputs, so once
     // all n bytes are in, the mailbox is free for the next call
     auto t0 = std::chrono::steady_clock::now();
