@@ -158,6 +158,27 @@ PBFTV_HD void fs_sqr_sub2(fe& r, const fe& a, const fe& b, const fe& c) {
   r.v[8] = r.v[8] - b.v[8] - (c.v[8] << 1);  // limb 8 of b and c: column 17, the output's top limb
 }
 
+// r = (a^2 + b c) 2^-261 (mod p): a squaring and a product under ONE
+// reduction.  a D-type (cross terms by the doubled limb: < 2^59, at most 4 per
+// column plus the square), b and c S-type (9 products < 2^58 per column): the
+// columns stay below 2^62.2 before the digit terms, as in fs_mul2_add.  Digit
+// step i follows row i: column i then holds every term of both parts.
+PBFTV_HD void fs_sqr_mul_add(fe& r, const fe& a, const fe& b, const fe& c) {
+  PBFTV_FS_CONSTS;
+  uint64_t t[17];
+  uint32_t a2[9];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) a2[i] = a.v[i] << 1;
+  fs_cols_init(t);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) {
+    t[2 * i] += smul(a.v[i], a.v[i]);
+    PBFTV_UNROLL for (int j = i + 1; j < 9; ++j) t[i + j] += smul(a.v[i], a2[j]);
+    PBFTV_UNROLL for (int j = 0; j < 9; ++j) t[i + j] += smul(b.v[i], c.v[j]);
+    if (i < 8) fs_digit(t, i, c8, c9, c18, c21, c24);
+    else fs_digit_top(t, c9, c18, c21, c24);
+  }
+  fs_out(r, t);
+}
+
 // r = a - b limb-wise (D-type for S-type inputs)
 PBFTV_HD void fs_sub(fe& r, const fe& a, const fe& b) {
   PBFTV_UNROLL for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] - b.v[i];
@@ -252,6 +273,59 @@ PBFTV_HD void xyzz_madd_s_flip(xyzz_s& acc, const fe& x2, const fe& y2) {
   fs_mul(acc.zz, acc.zz, pp);          // ZZ3 = ZZ1 PP
   fs_mul(acc.zzz, acc.zzz, ppp);       // ZZZ3 = ZZZ1 PPP
   acc.x = x3;
+}
+
+// ---- the comb's first and last additions (k_ecdsa_comb, comb2_verify) -------
+// First: the first two table points are both affine (ZZ1 = ZZZ1 = 1), so
+// U2 = x1, S2 = s1 y1, ZZ3 = PP and ZZZ3 = PPP: 4 products fewer than
+// xyzz_madd_s_flip.  (x0, s0 y0) + (x1, s1 y1) for canonical table coordinates
+// x0, y0, x1, y1 and flip = (s0 != s1).  With e = s0 s1 y0 and d = y1 - e
+// (R = s1 d), the result holds W = -s1 Y3 = d (X3 - Q) + e PPP: the caller's
+// sigma is -s1.  P = 0 (the two points equal or opposite) leaves ZZ = ZZZ = 0,
+// which later additions keep (the caller's exceptional-step test).
+PBFTV_HD void xyzz_aff_aff_s(xyzz_s& acc, const fe& x0, const fe& y0, const fe& x1, const fe& y1, bool flip) {
+  fe e, dy, d, p, pp, ppp, q, x3, t;
+  fs_cneg(e, y0, flip);                // e = s0 s1 y0            D
+  fs_sub(dy, y1, e);                   // |limbs| < 2^30
+  fs_norm(d, dy);                      // d                       S
+  fs_sub(p, x1, x0);                   // P = x1 - x0             D
+  fs_sqr(pp, p);
+  fs_mul(ppp, p, pp);
+  fs_mul(q, x0, pp);
+  fs_sqr_sub2(x3, d, ppp, q);          // X3 = d^2 - PPP - 2Q     S
+  fs_sub(t, x3, q);                    // X3 - Q                  D
+  fs_mul2_add(acc.y, d, t, e, ppp);    // W = d (X3 - Q) + e PPP  S
+  acc.x = x3;
+  acc.zz = pp;
+  acc.zzz = ppp;
+}
+
+// Last: the last addition is never formed.  Its x check X3 == r ZZ3 is
+//   R^2 - PPP - 2Q == r ZZ1 PP  <=>  R^2 - PP (P + 2 X1 + r ZZ1) == 0,
+// and P + 2 X1 = U2 + X1, so one squaring and one product under one reduction
+// (fs_sqr_mul_add) replace PPP, Q, X3, Y3, ZZ3, ZZZ3 and the check's r ZZ3.
+// xyzz_last_prep_s keeps what both candidates r and r + n share.
+struct xyzz_last_s {
+  fe p, rr, pp, base;  // P (D), R' = sigma R (D), PP (S), U2 + X1 (limbs < 2^30)
+};
+
+PBFTV_HD void xyzz_last_prep_s(xyzz_last_s& L, const xyzz_s& acc, const fe& x2, const fe& y2) {
+  fe u2, s2;
+  fs_mul(u2, x2, acc.zz);
+  fs_mul(s2, y2, acc.zzz);
+  fs_sub(L.p, u2, acc.x);
+  fs_sub(L.rr, s2, acc.y);
+  fs_sqr(L.pp, L.p);
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) L.base.v[i] = u2.v[i] + acc.x.v[i];
+}
+
+// d = (R^2 - PP (U2 + X1 + rz)) 2^-261 for rz = r ZZ1 (S-type): zero (mod p)
+// iff the sum's x coordinate is r, given ZZ1 != 0 and P != 0
+PBFTV_HD void xyzz_last_d_s(fe& d, const xyzz_last_s& L, const fe& rz) {
+  fe w, wn;
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) w.v[i] = 0u - L.base.v[i] - rz.v[i];  // (-3 2^29, 0]
+  fs_norm(wn, w);                                                                // S
+  fs_sqr_mul_add(d, L.rr, L.pp, wn);
 }
 
 }  // namespace pbftv

@@ -19,6 +19,8 @@
 // Compiled by hipcc for the GPU kernels, and by g++ for the CPU test harness
 // (tests/cpp) only.
 #pragma once
+#include <type_traits>
+
 #include "fe29.h"
 #include "fes.h"
 #include "safegcd.h"
@@ -429,54 +431,6 @@ PBFTV_HD bool comb2_mult(jac& acc, const uint32_t u1[8], const uint32_t u2[8], L
   return ok;
 }
 
-// ---- fast pass in XYZZ coordinates ---------------------------------------------
-// The throughput path: the same joint comb with unchecked madd-2008-s
-// additions into one XYZZ accumulator (8M + 2S per addition instead of
-// 7M + 4S, and fewer serial carry chains).  Exceptional steps leave ZZ == 0
-// (xyzz_madd), and the caller then reruns the signature with comb2_pass<true>.
-// The table point of digit d (|d| - 1 selects the entry, sign(d) negates y)
-// added to the signed-limb XYZZ accumulator (fes.h); the first point is loaded.
-PBFTV_HD void comb_add_entry_xyzz(xyzz_s& acc, bool& inf, int d, const uint32_t ew[16]) {
-  fe x, y;
-  entry_to_fe(x, y, ew);
-  fs_cneg(y, y, d < 0);
-  if (inf) {
-    acc.x = x;
-    fs_norm(acc.y, y);
-    fe_set(acc.zz, kOneP);
-    fe_set(acc.zzz, kOneP);
-    inf = false;
-    return;
-  }
-  xyzz_madd_s(acc, x, y);
-}
-
-template <int WG, int WQ, class LoadG, class LoadQ>
-PBFTV_HD bool comb2_pass_xyzz(xyzz_s& acc, const uint32_t u1[8], const uint32_t u2[8], LoadG load_g, LoadQ load_q) {
-  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
-  constexpr int nW = nG > nQ ? nG : nQ;
-  bool inf = true;
-  int c1 = 0, c2 = 0;
-  for (int i = 0; i < nW; ++i) {
-    uint32_t ew[16];
-    if (i < nG) {
-      const int d1 = signed_digit_w<WG>(u1, i, c1);
-      if (d1 != 0) {
-        load_g(i, (d1 < 0 ? -d1 : d1) - 1, ew);
-        comb_add_entry_xyzz(acc, inf, d1, ew);
-      }
-    }
-    if (i < nQ) {
-      const int d2 = signed_digit_w<WQ>(u2, i, c2);
-      if (d2 != 0) {
-        load_q(i, (d2 < 0 ? -d2 : d2) - 1, ew);
-        comb_add_entry_xyzz(acc, inf, d2, ew);
-      }
-    }
-  }
-  return !inf;
-}
-
 // ---- final check --------------------------------------------------------------
 // Accept iff R is finite and R.x mod n == r, where R.x = X / D (Jacobian:
 // D = Z^2; XYZZ: D = ZZ):  X == r D (mod p), or X == (r + n) D when r + n < p.
@@ -544,19 +498,141 @@ PBFTV_HD bool ecdsa_check(const xyzz_s& R, bool finite, const uint32_t r_w[8]) {
   return false;
 }
 
-// Whole comb + check for one signature: XYZZ fast pass, complete-addition
-// Jacobian rerun when a step was exceptional (ZZ == 0).
+// ---- the throughput comb's schedule (k_ecdsa_comb; comb2_verify restates it) ---
+// Joint step order: step j of the nG + nQ additions takes the G entry of
+// window j/2 (j even) and the Q entry (j odd) while both tables have windows
+// left, then the longer table's remaining windows.  Steps 0 and 1 are G window
+// 0 and Q window 0.
+template <int WG, int WQ>
+struct CombSteps {
+  static constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
+  static constexpr int nMin = nG < nQ ? nG : nQ;
+  static constexpr int nD = nG + nQ;
+  // LDS digit storage: d - 1 fits int16 for W <= 16 (d in [-(2^15 - 1), 2^15])
+  using Digit = std::conditional_t<(CombGeom<WG>::kW > 16 || CombGeom<WQ>::kW > 16), int, short>;
+  PBFTV_HDM static constexpr bool is_q(int j) { return j < 2 * nMin ? (j & 1) != 0 : nQ > nG; }
+  PBFTV_HDM static constexpr int win(int j) { return j < 2 * nMin ? j >> 1 : j - nMin; }
+};
+
+// The accumulator is XYZZ on signed limbs with W = sigma Y (neg_y: sigma = -1;
+// xyzz_madd_s_flip).  Per signature:
+//   * the first two digits both non-zero (all but ~2^-20 of signatures): the
+//     accumulator starts as the affine sum of their points (comb_first2_s);
+//   * every further step adds its point (comb_step_s: the generic step, which
+//     also starts the accumulator when digits are zero);
+//   * the last digit non-zero: the last addition is fused with the x check
+//     (comb_last_check_s); otherwise the plain check of the accumulator.
+// A result of -1 means an exceptional step (a doubling or cancellation met by
+// the unchecked additions): the signature is redone with complete additions.
+PBFTV_HD void comb_first2_s(xyzz_s& acc, bool& neg_y, int d0, const uint32_t w0[16], int d1, const uint32_t w1[16]) {
+  fe x0, y0, x1, y1;
+  entry_to_fe(x0, y0, w0);
+  entry_to_fe(x1, y1, w1);
+  xyzz_aff_aff_s(acc, x0, y0, x1, y1, (d0 < 0) != (d1 < 0));
+  neg_y = d1 > 0;  // sigma = -s1
+}
+
+PBFTV_HD void comb_step_s(xyzz_s& acc, bool& inf, bool& neg_y, int d, const uint32_t w[16]) {
+  if (d == 0) return;
+  fe x, y;
+  entry_to_fe(x, y, w);
+  fs_cneg(y, y, (d < 0) != neg_y);  // sigma * (+-y): D-type (no carry chain)
+  if (inf) {
+    acc.x = x;
+    fs_norm(acc.y, y);
+    fe_set(acc.zz, kOneP);
+    fe_set(acc.zzz, kOneP);
+    inf = false;
+  } else {
+    xyzz_madd_s_flip(acc, x, y);  // Y3 comes back with the other sign
+    neg_y = !neg_y;
+  }
+}
+
+// acc finite, d != 0: 1 / 0 = accept / reject, -1 = exceptional (ZZ1 == 0 from
+// an earlier step, or P == 0: the last point equals the sum or its negative)
+PBFTV_HD int comb_last_check_s(const xyzz_s& acc, bool neg_y, int d, const uint32_t w[16], const uint32_t r_w[8]) {
+  fe x, y, rr, r2p, rz, dd;
+  entry_to_fe(x, y, w);
+  fs_cneg(y, y, (d < 0) != neg_y);
+  xyzz_last_s L;
+  xyzz_last_prep_s(L, acc, x, y);
+  if (fs_is_zero(acc.zz) || fs_is_zero(L.p)) return -1;
+  fe_from_words(rr, r_w);
+  fe_set(r2p, kR2P);
+  fs_mul(rr, rr, r2p);  // r in Montgomery form
+  fs_mul(rz, rr, acc.zz);
+  xyzz_last_d_s(dd, L, rz);
+  if (fs_is_zero(dd)) return 1;
+  if (words_lt(r_w, kPMinusN32)) {  // r + n < p
+    uint32_t rn[8];
+    uint64_t cy = 0;
+    for (int i = 0; i < 8; ++i) {
+      cy += (uint64_t)r_w[i] + kN32[i];
+      rn[i] = (uint32_t)cy;
+      cy >>= 32;
+    }
+    fe_from_words(rr, rn);
+    fs_mul(rr, rr, r2p);
+    fs_mul(rz, rr, acc.zz);
+    xyzz_last_d_s(dd, L, rz);
+    if (fs_is_zero(dd)) return 1;
+  }
+  return 0;
+}
+
+// Whole comb + check for one signature, in k_ecdsa_comb's schedule (the kernel
+// makes the first-pair and last-step choices per wave, which changes no
+// result: the generic step is exact for every digit pattern); complete-addition
+// Jacobian rerun when a step was exceptional.  out_path (optional): bit 0 first
+// pair, bit 1 fused last step, bit 2 rerun.
 template <int WG = 8, int WQ = 8, class LoadG, class LoadQ>
 PBFTV_HD bool comb2_verify(const uint32_t u1[8], const uint32_t u2[8], const uint32_t r_w[8], LoadG load_g,
-                           LoadQ load_q) {
+                           LoadQ load_q, int* out_path = nullptr) {
+  using S = CombSteps<WG, WQ>;
+  int dg[S::nD];
+  int c1 = 0, c2 = 0;
+  for (int j = 0; j < S::nD; ++j)
+    dg[j] = S::is_q(j) ? signed_digit_w<WQ>(u2, S::win(j), c2) : signed_digit_w<WG>(u1, S::win(j), c1);
+  auto load = [&](int j, uint32_t w[16]) {
+    const int idx = (dg[j] < 0 ? -dg[j] : dg[j]) - 1;
+    if (S::is_q(j)) load_q(S::win(j), idx, w);
+    else load_g(S::win(j), idx, w);
+  };
   xyzz_s A;
-  const bool fin = comb2_pass_xyzz<WG, WQ>(A, u1, u2, load_g, load_q);
-  if (fin && fs_is_zero(A.zz)) {
+  bool inf = true, neg_y = false;
+  uint32_t w0[16], w1[16];
+  int j0 = 0, path = 0;
+  if (dg[0] != 0 && dg[1] != 0) {
+    load(0, w0);
+    load(1, w1);
+    comb_first2_s(A, neg_y, dg[0], w0, dg[1], w1);
+    inf = false;
+    j0 = 2;
+    path |= 1;
+  }
+  const bool fuse = j0 == 2 && dg[S::nD - 1] != 0;
+  for (int j = j0; j < (fuse ? S::nD - 1 : S::nD); ++j) {
+    if (dg[j] == 0) continue;
+    load(j, w0);
+    comb_step_s(A, inf, neg_y, dg[j], w0);
+  }
+  int res;
+  if (fuse) {
+    load(S::nD - 1, w0);
+    res = comb_last_check_s(A, neg_y, dg[S::nD - 1], w0, r_w);
+    path |= 2;
+  } else {
+    res = (!inf && fs_is_zero(A.zz)) ? -1 : (ecdsa_check(A, !inf, r_w) ? 1 : 0);
+  }
+  if (res < 0) {
+    path |= 4;
     jac R;
     const bool f2 = comb2_pass<true, WG, WQ>(R, u1, u2, load_g, load_q);
-    return ecdsa_check(R, f2, r_w);
+    res = ecdsa_check(R, f2, r_w) ? 1 : 0;
   }
-  return ecdsa_check(A, fin, r_w);
+  if (out_path) *out_path = path;
+  return res == 1;
 }
 
 // ---- key validation + table construction -------------------------------------

@@ -87,12 +87,11 @@ __device__ __forceinline__ void entry_words(const uint4 e[4], uint32_t ew[16]) {
   }
 }
 
-// Acc = xyzz: the unchecked fast pass (comb_add_entry_xyzz); Acc = jac with
-// kCheck: the complete-addition rerun (comb_add_entry<true>).
+// the complete-addition rerun's step (comb_add_entry<true>)
 template <bool kCheck, class Acc>
 __device__ __forceinline__ void comb_dev_add(Acc& acc, bool& inf, int d, const uint32_t ew[16]) {
-  if constexpr (kCheck) comb_add_entry<true>(acc, inf, d, ew);
-  else comb_add_entry_xyzz(acc, inf, d, ew);
+  static_assert(kCheck, "only the complete-addition pass reads entries this way");
+  comb_add_entry<true>(acc, inf, d, ew);
 }
 
 template <bool kCheck, int WG, int WQ, class Acc>
@@ -145,20 +144,6 @@ __device__ __noinline__ bool comb2_checked_verify(const SigRec* __restrict__ rp,
   const bool fin = comb2_dev_pass<true, WG, WQ>(R, u1, u2, gtab, qtab);
   return ecdsa_check(R, fin, r);
 }
-
-// Joint comb schedule: step j of the nG + nQ additions takes the G entry of
-// window j/2 (j even) and the Q entry (j odd) while both tables have windows
-// left, then the longer table's remaining windows.
-template <int WG, int WQ>
-struct CombSteps {
-  static constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
-  static constexpr int nMin = nG < nQ ? nG : nQ;
-  static constexpr int nD = nG + nQ;
-  // LDS digit storage: d - 1 fits int16 for W <= 16 (d in [-(2^15 - 1), 2^15])
-  using Digit = std::conditional_t<(CombGeom<WG>::kW > 16 || CombGeom<WQ>::kW > 16), int, short>;
-  __host__ __device__ static constexpr bool is_q(int j) { return j < 2 * nMin ? (j & 1) != 0 : nQ > nG; }
-  __host__ __device__ static constexpr int win(int j) { return j < 2 * nMin ? j >> 1 : j - nMin; }
-};
 
 // y = d < 0 ? 2p - y : y, lazily (limbs < 2^30: a valid fe_mul input) -- a
 // per-lane mask select, no carry chain and no divergence.
@@ -246,10 +231,42 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
   const uint4* qtab = act ? qtabs[meta.x] : gtab;  // the key's own table allocation
   xyzz_s R;  // signed-limb accumulator (fes.h); R.y holds sigma Y (xyzz_madd_s_flip)
   bool inf = true, neg_y = false;  // neg_y: sigma = -1
-  int d = (int)sdig[0][t] + 1;
-  issue_entry_lds(sent, t, entry_ptr<WG>(gtab, 0, d));
+  // The schedule of p256_algo.h comb2_verify, chosen per WAVE: the first two
+  // points are added affine + affine and the last addition is fused with the
+  // x check unless a lane with a signature has a zero digit there (~2^-20 per
+  // signature: then the whole wave takes the generic steps, which are exact
+  // for every digit pattern).  Lanes without a signature have zero digits and
+  // compute on entry 0, unread.
+  const int d0 = (int)sdig[0][t] + 1, d1 = (int)sdig[1][t] + 1;
+  const bool first2 = __ballot(act && (d0 == 0 || d1 == 0)) == 0;
+  const bool fuse = first2 && __ballot(act && sdig[S::nD - 1][t] == -1) == 0;
+  int d, j0;
+  if (first2) {
+    // both entries straight into registers (one memory round trip for the two),
+    // step 2's entry into LDS behind them
+    const uint4* p0 = entry_ptr<WG>(gtab, 0, d0);
+    const uint4* p1 = entry_ptr<WQ>(qtab, 0, d1);
+    uint4 e0[4], e1[4];
+    PBFTV_UNROLL for (int k = 0; k < 4; ++k) {
+      e0[k] = p0[k];
+      e1[k] = p1[k];
+    }
+    d = (int)sdig[2][t] + 1;
+    issue_entry_lds(sent, t, S::is_q(2) ? entry_ptr<WQ>(qtab, S::win(2), d) : entry_ptr<WG>(gtab, S::win(2), d));
+    uint32_t w0[16], w1[16];
+    entry_words(e0, w0);
+    entry_words(e1, w1);
+    comb_first2_s(R, neg_y, d0, w0, d1, w1);
+    inf = false;
+    j0 = 2;
+  } else {
+    d = d0;
+    issue_entry_lds(sent, t, entry_ptr<WG>(gtab, 0, d));
+    j0 = 0;
+  }
+  const int jend = fuse ? S::nD - 1 : S::nD;
 #pragma unroll 1
-  for (int j = 0; j < S::nD; ++j) {
+  for (int j = j0; j < jend; ++j) {
     uint32_t w16[16];
     read_entry_lds(sent, t, w16);
     const int dc = d;
@@ -258,30 +275,21 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
       issue_entry_lds(sent, t, S::is_q(j + 1) ? entry_ptr<WQ>(qtab, S::win(j + 1), d)
                                               : entry_ptr<WG>(gtab, S::win(j + 1), d));
     }
-    if (dc != 0) {
-      fe x, y;
-      entry_to_fe(x, y, w16);
-      fs_cneg(y, y, (dc < 0) != neg_y);  // sigma * (+-y): D-type (no carry chain)
-      if (inf) {
-        R.x = x;
-        fs_norm(R.y, y);
-        fe_set(R.zz, kOneP);
-        fe_set(R.zzz, kOneP);
-        inf = false;
-      } else {
-        xyzz_madd_s_flip(R, x, y);  // Y3 comes back with the other sign
-        neg_y = !neg_y;
-      }
-    }
+    comb_step_s(R, inf, neg_y, dc, w16);
   }
   if (act) {
-    if (!inf && fs_is_zero(R.zz)) {
-      ok = comb2_checked_verify<WG, WQ>(rp, gtab, qtab);  // exceptional step: redo
+    const uint4 e = rp->q[4], f = rp->q[5];
+    const uint32_t r[8] = {e.x, e.y, e.z, e.w, f.x, f.y, f.z, f.w};
+    int res;
+    if (fuse) {
+      uint32_t w16[16];
+      read_entry_lds(sent, t, w16);  // the last step's entry
+      res = comb_last_check_s(R, neg_y, d, w16, r);
     } else {
-      const uint4 e = rp->q[4], f = rp->q[5];
-      const uint32_t r[8] = {e.x, e.y, e.z, e.w, f.x, f.y, f.z, f.w};
-      ok = ecdsa_check(R, !inf, r);
+      res = (!inf && fs_is_zero(R.zz)) ? -1 : (ecdsa_check(R, !inf, r) ? 1 : 0);
     }
+    // exceptional step: redo with complete additions
+    ok = res < 0 ? comb2_checked_verify<WG, WQ>(rp, gtab, qtab) : res == 1;
   }
   if (okb != nullptr) {  // key order: one byte at the signature's own index, k_pack_bits builds the bitmap
     if (p < n) okb[meta.y] = ok ? 1 : 0;

@@ -174,6 +174,23 @@ int h_verify_w(int w, const uint8_t* hash, const uint8_t* rs, const uint32_t* gt
   return ok ? 1 : 0;
 }
 
+// comb2_verify (k_ecdsa_comb's schedule) on chosen scalars u1, u2 and r (LE
+// words) with (w, w) tables; *path: bit 0 first pair, 1 fused last step, 2 rerun
+int h_comb_verify_u(int w, const uint32_t* u1, const uint32_t* u2, const uint32_t* r, const uint32_t* gtab,
+                    const uint32_t* qtab, int* path) {
+  bool ok = false;
+  auto run = [&](auto geom) {
+    constexpr int W = decltype(geom)::kCode;
+    auto lg = [&](int win, int idx, uint32_t* out) { memcpy(out, gtab + (CombGeom<W>::base(win) + idx) * 16, 64); };
+    auto lq = [&](int win, int idx, uint32_t* out) { memcpy(out, qtab + (CombGeom<W>::base(win) + idx) * 16, 64); };
+    ok = comb2_verify<W, W>(u1, u2, r, lg, lq, path);
+  };
+  if (w == 8) run(CombGeom<8>());
+  else if (w == 11) run(CombGeom<11>());
+  else return -1;
+  return ok ? 1 : 0;
+}
+
 // ---- signed-limb arithmetic (fes.h) ----
 void h_fs_mul(const uint32_t* a, const uint32_t* b, uint32_t* r) {
   fe x, y, z;
@@ -198,6 +215,26 @@ void h_fs_sqr_sub2(const uint32_t* a, const uint32_t* b, const uint32_t* c, uint
   memcpy(x.v, a, 36); memcpy(y.v, b, 36); memcpy(u.v, c, 36);
   fs_sqr_sub2(z, x, y, u);
   memcpy(r, z.v, 36);
+}
+void h_fs_sqr_mul_add(const uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t* r) {
+  fe x, y, u, z;
+  memcpy(x.v, a, 36); memcpy(y.v, b, 36); memcpy(u.v, c, 36);
+  fs_sqr_mul_add(z, x, y, u);
+  memcpy(r, z.v, 36);
+}
+// pts = x0 || y0 || x1 || y1 (canonical limbs, 36 words); acc out as in h_xyzz_madd_s
+void h_xyzz_aff_aff_s(const uint32_t* pts, int flip, uint32_t* acc) {
+  fe x0, y0, x1, y1;
+  memcpy(x0.v, pts, 36); memcpy(y0.v, pts + 9, 36); memcpy(x1.v, pts + 18, 36); memcpy(y1.v, pts + 27, 36);
+  xyzz_s A;
+  xyzz_aff_aff_s(A, x0, y0, x1, y1, flip != 0);
+  memcpy(acc, A.x.v, 36); memcpy(acc + 9, A.y.v, 36); memcpy(acc + 18, A.zz.v, 36); memcpy(acc + 27, A.zzz.v, 36);
+}
+// the fused last step: acc (36 words), the entry's canonical words (16), digit d, r (LE words)
+int h_comb_last_check_s(const uint32_t* acc, int neg_y, int d, const uint32_t* w16, const uint32_t* r) {
+  xyzz_s A;
+  memcpy(A.x.v, acc, 36); memcpy(A.y.v, acc + 9, 36); memcpy(A.zz.v, acc + 18, 36); memcpy(A.zzz.v, acc + 27, 36);
+  return comb_last_check_s(A, neg_y != 0, d, w16, r);
 }
 void h_fs_norm(const uint32_t* a, uint32_t* r) {
   fe x, z;

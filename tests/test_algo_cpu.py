@@ -486,6 +486,164 @@ def test_xyzz_madd_s_flip_chain(H):
         assert sval(a2[18:27]) % P == 0 and sval(a2[27:36]) % P == 0
 
 
+def test_fs_sqr_mul_add_types_and_values(H):
+    """fs_sqr_mul_add (the fused last step's R^2 + PP W under one reduction):
+    a D-type, b and c S-type, random and at the type bounds: the Montgomery
+    value, S-type output."""
+    rng = np.random.default_rng(0x5A11)
+    out = (ctypes.c_uint32 * 9)()
+    Rinv = pow(R, -1, P)
+    for it in range(3000):
+        ext = it % 4 == 0
+        (la, a), (lb, b), (lc, c) = rand_d(rng, ext), rand_s(rng, ext), rand_s(rng, ext)
+        H.h_fs_sqr_mul_add(slimbs(la), slimbs(lb), slimbs(lc), out)
+        v = check_s(out)
+        assert v % P == (a * a + b * c) * Rinv % P
+    # the fused step's multiplicand: fs_norm of -(U2 + X1 + rz), limbs in (-3 2^29, 0]
+    for _ in range(500):
+        parts = [rand_s(rng, bool(rng.integers(0, 2))) for _ in range(3)]
+        w = [-(parts[0][0][i] + parts[1][0][i] + parts[2][0][i]) for i in range(9)]
+        H.h_fs_norm(slimbs(w), out)
+        assert sval(out) == -(parts[0][1] + parts[1][1] + parts[2][1])
+        assert all(0 <= int(x) < (1 << 29) for x in out[:8]) and abs(sval(out[8:9])) < (1 << 28)
+
+
+def _mont(v):
+    return v * R % P
+
+
+def _unmont(v):
+    return v * pow(R, -1, P) % P
+
+
+def test_xyzz_aff_aff_s_first_pair(H):
+    """The comb's first step (fes.h xyzz_aff_aff_s): the affine sum of the first
+    two table points, for every sign pair; W carries sigma = -s1; equal or
+    opposite points leave ZZ = ZZZ = 0."""
+    from oracle import p256
+    rng = np.random.default_rng(73)
+    acc = (ctypes.c_uint32 * 36)()
+    for it in range(300):
+        a = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+        b = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+        s0, s1 = int(rng.choice([-1, 1])), int(rng.choice([-1, 1]))
+        pts = (ctypes.c_uint32 * 36)(*limbs(_mont(a[0])), *limbs(_mont(a[1])), *limbs(_mont(b[0])), *limbs(_mont(b[1])))
+        H.h_xyzz_aff_aff_s(pts, int(s0 != s1), acc)
+        for k in range(4):
+            check_s(acc[9 * k:9 * k + 9])
+        x, w, zz, zzz = (_unmont(sval(acc[9 * k:9 * k + 9]) % P) for k in range(4))
+        want = p256.point_add((a[0], a[1] if s0 > 0 else P - a[1]), (b[0], b[1] if s1 > 0 else P - b[1]))
+        assert (x * pow(zz, -1, P) % P, -s1 * w * pow(zzz, -1, P) % P) == want, it
+    a = p256.scalar_mult(12345, p256.G)
+    for s0, s1 in ((1, 1), (1, -1)):  # the same point twice: doubling (or its negative: infinity)
+        pts = (ctypes.c_uint32 * 36)(*limbs(_mont(a[0])), *limbs(_mont(a[1])), *limbs(_mont(a[0])), *limbs(_mont(a[1])))
+        H.h_xyzz_aff_aff_s(pts, int(s0 != s1), acc)
+        assert sval(acc[18:27]) % P == 0 and sval(acc[27:36]) % P == 0
+
+
+def _w11_digits(u):
+    """signed recoding of the mixed W = 11 code (15 x 12 + 7 x 11 bits)"""
+    out, c = [], 0
+    for i in range(22):
+        wd, bit = (12, 12 * i) if i < 15 else (11, 180 + 11 * (i - 15))
+        d = ((u >> bit) & ((1 << wd) - 1)) + c
+        c = 1 if d > (1 << (wd - 1)) else 0
+        out.append((d - (c << wd), bit))
+    return out
+
+
+def test_comb_schedule_first_pair_fused_last_rerun(H):
+    """p256_algo.h comb2_verify -- k_ecdsa_comb's schedule: first pair added
+    affine + affine, last addition fused with the x check, complete-addition
+    rerun -- on chosen (u1, u2, r) with Q = G on the mixed W = 11 tables:
+      * random scalars, r = R.x mod n (accept) and r off by one (reject): path
+        first pair + fused;
+      * a zero first digit (then the generic steps throughout) and a zero
+        last digit (the plain check): same bits;
+      * the last point equal to the sum before it (doubling) or its negative
+        (cancellation): the fused step reports it, the rerun decides;
+      * r + n < p: the second candidate of the fused check."""
+    from oracle import p256
+    words = (15 * 2048 + 7 * 1024) * 16
+    g = (ctypes.c_uint32 * words)()
+    assert H.h_build_table_w(None, 11, g) == 1
+    W = ctypes.c_uint32 * 8
+    path = ctypes.c_int()
+
+    def w8(v):
+        return W(*[(v >> 32 * i) & 0xFFFFFFFF for i in range(8)])
+
+    def run(u1, u2, r):
+        ok = H.h_comb_verify_u(11, w8(u1), w8(u2), w8(r), g, g, ctypes.byref(path))
+        assert ok in (0, 1)
+        return bool(ok), path.value
+
+    def rx(u):
+        pt = p256.scalar_mult(u % N, p256.G)
+        return None if pt is None else pt[0] % N
+
+    rng = np.random.default_rng(74)
+    for _ in range(40):
+        u1, u2 = (int.from_bytes(rng.bytes(32), "big") % N for _ in range(2))
+        r = rx(u1 + u2)
+        assert run(u1, u2, r) == (True, 3)
+        assert run(u1, u2, (r + 1) % N or 1) == (False, 3)
+    # zero digits at the ends: u1 with a zero lowest window, u2 with a zero top window
+    u1 = (int.from_bytes(rng.bytes(32), "big") % N) & ~0xFFF
+    u2 = int.from_bytes(rng.bytes(32), "big") % N
+    assert _w11_digits(u1)[0][0] == 0
+    assert run(u1, u2, rx(u1 + u2)) == (True, 0)  # no first pair: no fused step either (the kernel's rule)
+    u2s = int.from_bytes(rng.bytes(28), "big")
+    assert _w11_digits(u2s)[-1][0] == 0
+    assert run(u1 | 1, u2s, rx((u1 | 1) + u2s)) == (True, 1)
+    # the last point meets the sum before it: u1 + u2 - d 2^b = +-d 2^b
+    hits = 0
+    for _ in range(40):
+        u2 = int.from_bytes(rng.bytes(32), "big") % N
+        d, b = _w11_digits(u2)[-1]
+        if d == 0:
+            continue
+        hits += 1
+        t = d * (1 << b)
+        u1 = (2 * t - u2) % N  # sum R = 2T: a doubling at the last step
+        r = rx(u1 + u2)
+        ok, pth = run(u1, u2, r)
+        assert ok and pth & 4, pth
+        ok, pth = run(u1, u2, (r + 1) % N)
+        assert not ok and pth & 4
+        u1 = (-u2) % N  # R = infinity: a cancellation at the last step
+        ok, pth = run(u1, u2, 1)
+        assert not ok and pth & 4
+    assert hits > 30
+    # r + n < p: a sum whose x lies in [n, p) is accepted for r = x - n, by
+    # the fused check's second candidate.  No scalar reaches such a point in a
+    # test's time (2^-128), so the step runs on a chosen accumulator A = S - T
+    # (random Z) and entry T, for a point S with x in [n, p).
+    B = 0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B
+    acc = (ctypes.c_uint32 * 36)()
+    ew = (ctypes.c_uint32 * 16)()
+    tried = 0
+    for xs in range(N + 1, N + 2000):
+        rhs = (xs ** 3 - 3 * xs + B) % P
+        ys = pow(rhs, (P + 1) // 4, P)
+        if ys * ys % P != rhs:
+            continue
+        tried += 1
+        t = p256.scalar_mult(int(rng.integers(1, 2 ** 62)), p256.G)
+        a = p256.point_add((xs, ys), (t[0], (P - t[1]) % P))
+        z = int(rng.integers(2, 2 ** 62))
+        for k, v in enumerate((a[0] * z * z, a[1] * z ** 3, z * z, z ** 3)):
+            acc[9 * k:9 * k + 9] = list(limbs(_mont(v % P)))
+        ew[:8] = [(_mont(t[0]) >> 32 * i) & 0xFFFFFFFF for i in range(8)]
+        ew[8:] = [(_mont(t[1]) >> 32 * i) & 0xFFFFFFFF for i in range(8)]
+        assert H.h_comb_last_check_s(acc, 0, 1, ew, w8(xs - N)) == 1
+        assert H.h_comb_last_check_s(acc, 0, 1, ew, w8(xs - N + 1)) == 0
+        assert H.h_comb_last_check_s(acc, 0, -1, ew, w8(xs - N)) == 0  # the entry negated: another sum
+        if tried == 5:
+            break
+    assert tried == 5
+
+
 # ---- lane-parallel safegcd of the latency path (verify_kernels.h inv_mod_n_wave) ----
 # A restatement of the kernel's scheme with exact integers: one list entry per
 # lane-limb, 30-bit signed limbs re-centered after every batch, divsteps on the
