@@ -50,9 +50,12 @@ METRIC = "sig verifies/sec at 1/2/4/8 MI355X; p50 quorum-cert verify latency"
 # (one v_mad_u64_u32).  fe_mul 81, fe_sqr 45, fn_mul 81 + 81 (n-reduction).
 N_ORDER = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
 FE_MUL, FE_SQR, FN_MUL = 81, 45, 162
-MADD = 8 * FE_MUL + 2 * FE_SQR                     # XYZZ madd-2008-s (p256_algo.h xyzz_madd)
+MADD = 8 * FE_MUL + 2 * FE_SQR                     # XYZZ madd-2008-s (fes.h xyzz_madd_s_flip)
+AFF_ADD = 4 * FE_MUL + 2 * FE_SQR                  # first pair, affine + affine (fes.h xyzz_aff_aff_s)
+LAST_ADD = 4 * FE_MUL + 2 * FE_SQR                 # last addition fused with the x check (fes.h xyzz_last_*):
+                                                   # U2, S2, PP, r ZZ1, R^2 + PP W under one reduction
 JADD = 12 * FE_MUL + 4 * FE_SQR                    # add-2007-bl (final complete add)
-CHECK = 2 * FE_MUL                                  # X == r ZZ test: r to Montgomery form, r ZZ
+CHECK = FE_MUL                                      # r to Montgomery form (r ZZ1 is in LAST_ADD)
 
 
 def window_widths(code: int) -> list:
@@ -68,8 +71,10 @@ def window_widths(code: int) -> list:
 
 
 def macs_comb(gbits: int, qbits: int) -> float:
-    """Joint comb (p256_kernels.hip k_ecdsa_comb): one mixed addition per nonzero
-    signed digit of u1 (G table) and u2 (key table), minus the first (a load).
+    """Joint comb (verify_kernels.h k_ecdsa_comb, schedule p256_algo.h
+    comb2_verify): one addition per nonzero signed digit of u1 (G table) and u2
+    (key table) but the first (a load); of those, the first is affine + affine
+    and the last is fused with the x check, the rest are mixed XYZZ additions.
     Windows below 256 bits are nonzero w.p. 1 - 2^-W; the top (carry) window
     w.p. ~1/2 when 256 % W == 0, else its 256 % W real bits make it nonzero."""
     def nonzero(w):
@@ -77,7 +82,7 @@ def macs_comb(gbits: int, qbits: int) -> float:
         top_bits = 256 - sum(ws[:-1])
         top = 0.5 if top_bits <= 0 else 1.0
         return sum(1 - 2.0 ** -x for x in ws[:-1]) + top
-    return (nonzero(gbits) + nonzero(qbits) - 1) * MADD + CHECK
+    return (nonzero(gbits) + nonzero(qbits) - 3) * MADD + AFF_ADD + LAST_ADD + CHECK
 
 
 # safegcd inversion (safegcd.h): at most 25 batches of 30 divsteps, each applying

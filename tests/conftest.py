@@ -114,6 +114,36 @@ def oracle_sign_pool(oracle_lib, n_keys: int, per_key: int, seed: int):
     return keys, hashes, sigs, kidx
 
 
+def signed_digits(u: int, widths) -> list:
+    """Signed recoding of u over windows of the given widths (p256_algo.h
+    signed_digit_w): [(digit, start bit)]."""
+    out, c, bit = [], 0, 0
+    for wd in widths:
+        d = ((u >> bit) & ((1 << wd) - 1)) + c
+        c = 1 if d > (1 << (wd - 1)) else 0
+        out.append((d - (c << wd), bit))
+        bit += wd
+    return out
+
+
+def chosen_scalar_sig(u1: int, u2: int, flip_r: bool = False):
+    """A signature under the key Q = G whose verify recomputes exactly (u1, u2):
+    R = (u1 + u2) G, r = x(R) mod n (r = 1 when R is infinity: rejected),
+    s = r / u2, e = u1 s.  Returns (hash, r||s, expected accept bit)."""
+    from oracle import p256
+    N = p256.N
+    R = p256.scalar_mult((u1 + u2) % N, p256.G)
+    r = 1 if R is None else R[0] % N
+    s = r * pow(u2, -1, N) % N
+    e = u1 * s % N
+    h = e.to_bytes(32, "big")
+    if flip_r:
+        r ^= 2
+    rs = r.to_bytes(32, "big") + s.to_bytes(32, "big")
+    return (np.frombuffer(h, np.uint8), np.frombuffer(rs, np.uint8),
+            p256.verify(h, r, s, p256.GX, p256.GY))
+
+
 def crafted_exceptional():
     """Valid signatures with chosen (u1, u2) under the key Q = G: pick u1, u2,
     R = (u1 + u2) G, r = x(R) mod n, s = r / u2, e = u1 s (the verifier then
