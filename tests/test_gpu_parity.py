@@ -364,6 +364,52 @@ def test_host_pipeline_chunks_pageable_and_pinned(ver, oracle_lib, chunk, layout
     assert (np.unpackbits(want, bitorder="little")[:m].astype(bool) == got[:m]).all()
 
 
+@pytest.mark.parametrize("chunk", ["4096", "262144"])
+def test_host_pipeline_concurrent_callers(ver, oracle_lib, chunk, monkeypatch):
+    """Concurrent host-buffer calls on one context (a Go node's pools flushing
+    at once; the cgo pattern of tests/cpp/test_cgo_pattern.cpp, here on the
+    chunked large-batch path): three threads, different batch sizes and
+    corruption masks, pageable and pinned inputs, many chunks (4096) and few
+    (262144), so device slots, key and bitmap buffers are reused call after
+    call: every call's bitmap must be its own batch's."""
+    import threading
+    monkeypatch.setenv("PBFTV_HOST_CHUNK", chunk)
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=16, per_key=32, seed=61)
+    ver.register_keys(keys)
+    rng = np.random.default_rng(62)
+    jobs = []
+    for t, n in enumerate((30_000 + 77, 52_224, 12_289)):
+        o = rng.integers(0, len(kidx), n)
+        H, S, K = hashes[o].copy(), sigs[o].copy(), kidx[o].copy()
+        bad = rng.random(n) < (0.01, 0.2, 0.5)[t]
+        S[np.nonzero(bad)[0], 33] ^= 8
+        jobs.append((H, S, K, ~bad))
+    pins = [ver.pinned(a) for a in jobs[1][:3]]
+    jobs[1] = (*(p.a for p in pins), jobs[1][3])
+    errors = []
+
+    def run(job):
+        try:
+            for _ in range(6):
+                got = ver.verify_batch(*job[:3])
+                if not (got == job[3]).all():
+                    errors.append(int((got != job[3]).sum()))
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append(repr(e))
+
+    try:
+        th = [threading.Thread(target=run, args=(j,)) for j in jobs]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+        assert not any(x.is_alive() for x in th)
+        assert errors == []
+    finally:
+        for p in pins:
+            p.free()
+
+
 def test_dev_calls_on_two_streams_share_scratch(ver, oracle_lib, monkeypatch):
     """*_dev calls on a caller stream and on the context stream reuse
     the device scratch (scalars, flags, key order); the scratch event orders
