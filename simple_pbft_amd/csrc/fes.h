@@ -214,11 +214,19 @@ PBFTV_HD void fs_canon(fe& r, const fe& a) {
   fe_canon(r, n);
 }
 
+// a == 0 (mod p) for an S- or D-type value, without the canonical subtract:
+// fe_fold_carry subtracts top p (top = (limb 8 - 4) >> 24, |top| <= 5) and
+// leaves limb 8 in [4, 2^24 + 4), so the folded value lies in (2^233, 2^256 +
+// 2^235) -- strictly inside (0, 2p) -- and its only multiple of p is p itself:
+// zero iff the folded digits are p's (tests/test_algo_cpu.py checks the range
+// and every multiple k p, |k| <= 5, in S- and D-type form).
 PBFTV_HD bool fs_is_zero(const fe& a) {
-  fe c;
-  fs_canon(c, a);
+  int32_t d[9];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) d[i] = (int32_t)a.v[i];
+  fe n;
+  fe_fold_carry(n, d);
   uint32_t o = 0;
-  PBFTV_UNROLL for (int i = 0; i < 9; ++i) o |= c.v[i];
+  PBFTV_UNROLL for (int i = 0; i < 9; ++i) o |= n.v[i] ^ kP[i];
   return o == 0;
 }
 

@@ -236,6 +236,19 @@ int h_comb_last_check_s(const uint32_t* acc, int neg_y, int d, const uint32_t* w
   memcpy(A.x.v, acc, 36); memcpy(A.y.v, acc + 9, 36); memcpy(A.zz.v, acc + 18, 36); memcpy(A.zzz.v, acc + 27, 36);
   return comb_last_check_s(A, neg_y != 0, d, w16, r);
 }
+int h_fs_is_zero(const uint32_t* a) {
+  fe x;
+  memcpy(x.v, a, 36);
+  return fs_is_zero(x) ? 1 : 0;
+}
+// the fold of fs_is_zero (fe_fold_carry) on S/D-type limbs
+void h_fs_fold(const uint32_t* a, uint32_t* r) {
+  int32_t d[9];
+  memcpy(d, a, 36);
+  fe n;
+  fe_fold_carry(n, d);
+  memcpy(r, n.v, 36);
+}
 void h_fs_norm(const uint32_t* a, uint32_t* r) {
   fe x, z;
   memcpy(x.v, a, 36);

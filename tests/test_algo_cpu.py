@@ -508,6 +508,38 @@ def test_fs_sqr_mul_add_types_and_values(H):
         assert all(0 <= int(x) < (1 << 29) for x in out[:8]) and abs(sval(out[8:9])) < (1 << 28)
 
 
+def test_fs_is_zero_fold_range(H):
+    """fes.h fs_is_zero: fe_fold_carry of an S- or D-type value lies strictly
+    inside (0, 2p), so the value is 0 mod p iff the folded digits are p's.
+    Random and type-bound values, every multiple k p (|k| <= 5) written as an
+    S-type value and as D-type differences of two S-type values."""
+    rng = np.random.default_rng(0x2E40)
+    out = (ctypes.c_uint32 * 9)()
+
+    def check(l, v):
+        H.h_fs_fold(slimbs(l), out)
+        f = val(out)
+        assert all(0 <= int(x) < (1 << 29) for x in out[:8])
+        assert 0 < f < 2 * P and f % P == v % P, (l, v)
+        assert H.h_fs_is_zero(slimbs(l)) == (1 if v % P == 0 else 0)
+
+    for it in range(4000):
+        (l, v) = (rand_s if it % 2 else rand_d)(rng, it % 3 == 0)
+        check(l, v)
+    for k in range(-5, 6):
+        v = k * P
+        if abs(v) < S_BOUND:
+            check(s_limbs_of(v), v)
+        for _ in range(50):
+            a, va = rand_s(rng, False)
+            wb = va - v  # b = a - k p: a - b = k p as limb-wise difference
+            if abs(wb) >= S_BOUND:
+                continue
+            b = s_limbs_of(wb)
+            check([x - y for x, y in zip(a, b)], v)
+            check([x - y for x, y in zip(a, b)][:8] + [a[8] - b[8] + 1], v + (1 << 232))  # one off
+
+
 def _mont(v):
     return v * R % P
 
