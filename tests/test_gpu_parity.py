@@ -447,6 +447,34 @@ def test_dev_calls_on_two_streams_share_scratch(ver, oracle_lib, monkeypatch):
 
 
 # ---- the armed latency kernel (pbftv_api.cpp qc_arm / k_ecdsa_wave_armed) ----
+def test_armed_path_golden_and_crafted(ecdsa_fixtures):
+    """Every golden vector (valid, high-S, the corruption classes, e >= n,
+    R.x >= n, invalid keys, the crafted doubling / cancellation sums) and the
+    chosen-scalar exceptional sums, served in calls of 1-8 signatures -- the
+    sizes the armed kernel takes from its mailbox slots -- against the
+    fixtures' expected bits."""
+    from conftest import crafted_exceptional
+    from simple_pbft_amd import Verifier
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    rng = np.random.default_rng(79)
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        o = rng.permutation(len(kidx))
+        at = 0
+        while at < len(o):
+            m = int(rng.integers(1, 9))
+            sel = o[at:at + m]
+            got = v.verify_batch(hashes[sel], sigs[sel], kidx[sel])
+            bad = [ecdsa_fixtures["vectors"][i]["kind"] for i, g in zip(sel, got) if g != expect[i]]
+            assert not bad, bad
+            at += m
+        key, H, S, K, E = crafted_exceptional()
+        v.register_keys(key)
+        for a in range(0, len(K), 4):
+            assert (v.verify_batch(H[a:a + 4], S[a:a + 4], K[a:a + 4]) == E[a:a + 4]).all(), a
+
+
+
 @pytest.mark.parametrize("arm_ms", ["500", "1"])
 def test_armed_latency_path(oracle_lib, arm_ms, monkeypatch):
     """Small host-buffer batches are served by the kernel armed at the end of
