@@ -15,5 +15,5 @@ cd "$ROOT"
 timeout -k 10 900 bash tools/pmc_passes.sh "$OUT/pmc" > "$OUT/pmc_passes.log" 2>&1 || { echo "pmc failed"; tail -20 "$OUT/pmc_passes.log"; exit 1; }
 python3 tools/pmc_summary.py "$OUT/pmc" > "$OUT/pmc_summary.json" 2> "$OUT/pmc_summary.err" || { echo "summary failed"; cat "$OUT/pmc_summary.err"; exit 1; }
 cat "$OUT/pmc_summary.json"
-find "$OUT/trace" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
+python3 tools/rocpd_stats.py "$OUT/trace/run_results.db" > "$OUT/kernel_stats.csv"  # rocpd SQLite output (ROCm 7)
 head -20 "$OUT/kernel_stats.csv"
