@@ -111,8 +111,11 @@ def macs_scalars(k: int) -> float:
     lane and across the wave over PLAIN s values, p256_kernels.hip k_ecdsa_scalars /
     wave_batch_inv_n): per signature u1, u2 (2 products) + 3 (k - 1) / k for the
     lane's prefix, back-substitution and running inverse; per lane 15 for the wave
-    scans and 2 (1 at k = 1) R-power fixes; 1/(64 k) of an inversion."""
+    scans and 2 (1 at k = 1) R-power fixes; 1/(64 k) of an inversion.  From k = 4
+    one scan and inversion per 256-thread block (block_batch_inv_n)."""
     per_sig = 2 + 3 * (k - 1) / k
+    if k >= 4:  # block_batch_inv_n: quad scans 4 + recovery 2 per lane, wave 0's 15 shared by 4 waves
+        return per_sig * FN_MUL + (6 + 15 / 4 + 2) * FN_MUL / k + INV_N_MACS / (256 * k)
     per_lane = 15 + (2 if k > 1 else 1)
     return per_sig * FN_MUL + per_lane * FN_MUL / k + INV_N_MACS / (64 * k)
 # v_mad_u64_u32 issue peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz (4-cycle wave64 issue);

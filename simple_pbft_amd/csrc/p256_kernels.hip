@@ -19,6 +19,10 @@
 namespace pbftv {
 
 // key-order sort (k_key_*): blocks of the histogram/scatter passes, largest key count sorted
+#ifndef PBFTV_SCAL_BLOCK_INV_MIN_K
+#define PBFTV_SCAL_BLOCK_INV_MIN_K 4  // K from which stage 1 inverts once per block (block_batch_inv_n)
+#endif
+
 #ifndef PBFTV_SCAL_WAVES
 #define PBFTV_SCAL_WAVES 1  // min waves per SIMD for k_ecdsa_scalars (the compiler settles at 124 VGPRs: 4)
 #endif
@@ -445,7 +449,8 @@ __device__ __forceinline__ void block_key_starts(const uint32_t* __restrict__ to
 //             inv = fn_mul(inv, s_j); w_0 = inv.
 // Per signature 4 Montgomery multiplies (c_j, w_j, inv, and u1 / u2: 2) + 16/K
 // for the lane fixes and the wave scans + 1/(64 K) of an inversion (round 2
-// converted every s: 6 + 14/K).
+// converted every s: 6 + 14/K); from K = 4 the scan and the inversion are
+// shared by the block (block_batch_inv_n): 2/K + 9.75/K and 1/(256 K).
 template <int K>
 __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const uint8_t* __restrict__ hashes,
                                                        const uint8_t* __restrict__ sigs,
@@ -528,8 +533,18 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
     __syncthreads();
   }
   fe inv;
-  wave_batch_inv_n(inv, acc);  // P^-1 R: one inversion per wave (64 K signatures; one per
-                               // 256-thread block measured slower: 0.126 vs 0.120 ms)
+  if constexpr (K >= PBFTV_SCAL_BLOCK_INV_MIN_K) {
+    // P^-1 R: one inversion and one cross-lane scan per 256-thread block, 6
+    // products per lane instead of 15 (kstart is free once the claims above
+    // are made; 64 x 9 words of it hold the quad products).  Same box, two
+    // streams: 1M step -0.3 %, 262k -1 %; at K <= 2 (131k, one wave round) the
+    // barriers lengthen the lone kernel (0.051 vs 0.046 ms), so K <= 2 keep
+    // one inversion per wave (profiles/r03_ab_block_inversion.txt)
+    static_assert(kSortMaxKeys + 1 >= 64 * 9, "kstart holds the block inversion's slots");
+    block_batch_inv_n(inv, acc, kstart);
+  } else {
+    wave_batch_inv_n(inv, acc);  // P^-1 R: one inversion per wave (64 K signatures)
+  }
   if (K > 1) {
     fe_set(rk, kRPowN[K]);
     fn_mul(inv, inv, rk);      // P^-1 R^K

@@ -921,6 +921,50 @@ __device__ __forceinline__ void wave_batch_inv_n(fe& inv, const fe& acc) {
   fn_mul(inv, a, invt);
 }
 
+// The same for a 256-thread block: the 4 waves' values are multiplied within
+// quads (lanes 4q .. 4q+3: inclusive prefix and suffix by two shuffle steps),
+// the 64 quad products go through LDS to wave 0, which alone runs
+// wave_batch_inv_n over them (one inversion and one cross-lane scan per BLOCK),
+// and each lane takes its inverse as quad^-1 * (prefix before it) * (suffix
+// after it).  Per lane 6 products (wave 0: + 15 and the inversion) instead of
+// 15 and an inversion per wave.  slots: >= 64 * 9 words of LDS; every thread
+// of the block calls this (two barriers).
+__device__ __forceinline__ void block_batch_inv_n(fe& inv, const fe& acc, uint32_t* slots) {
+  const int lane = (int)(threadIdx.x & 63u), q = lane & 3, wv = (int)(threadIdx.x >> 6);
+  const int slot = wv * 16 + (lane >> 2);
+  fe one, pre = acc, suf = acc, a, b;
+  fe_set(one, kOneN);
+  PBFTV_UNROLL for (int k = 1; k < 4; k <<= 1) {
+    shfl_fe(a, pre, lane - k);
+    shfl_fe(b, suf, lane + k);
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+      a.v[l] = q >= k ? a.v[l] : one.v[l];
+      b.v[l] = q + k < 4 ? b.v[l] : one.v[l];
+    }
+    fn_mul(pre, pre, a);  // inclusive prefix product within the quad
+    fn_mul(suf, suf, b);  // inclusive suffix product within the quad
+  }
+  if (q == 3) PBFTV_UNROLL for (int l = 0; l < 9; ++l) slots[l * 64 + slot] = pre.v[l];
+  __syncthreads();
+  if (wv == 0) {
+    fe x, y;
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) x.v[l] = slots[l * 64 + lane];
+    wave_batch_inv_n(y, x);  // the quad products' inverses (Montgomery form)
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) slots[l * 64 + lane] = y.v[l];
+  }
+  __syncthreads();
+  fe qi;
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) qi.v[l] = slots[l * 64 + slot];
+  shfl_fe(a, pre, lane - 1);
+  shfl_fe(b, suf, lane + 1);
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+    a.v[l] = q >= 1 ? a.v[l] : one.v[l];
+    b.v[l] = q < 3 ? b.v[l] : one.v[l];
+  }
+  fn_mul(a, a, b);
+  fn_mul(inv, a, qi);
+}
+
 // a b 2^-261 mod m with a per-lane modulus m (29-bit limbs) and mp = -m^-1 mod
 // 2^29: one step of the latency path runs mod-n and mod-p products side by
 // side on different lanes.  Inputs limbs < 2^29, a < 2^257, b < 2^261;
