@@ -652,9 +652,17 @@ def main():
         n = hi - lo
         pub, H, S, K, ok = synth.config4(n_global, n_keys=args.keys, seed=0x50424654)
         H, S, K, ok = H[lo:hi], S[lo:hi], K[lo:hi], ok[lo:hi]
-    t_reg = time.perf_counter()
-    valid = ver.register_keys(pub)
-    t_reg = time.perf_counter() - t_reg  # G table + one table per key, built on the device
+    if share:  # ranks sharing one GPU register one after the other: each sizes its tables from what is free
+        for r in range(ws):
+            if r == rank:
+                t_reg = time.perf_counter()
+                valid = ver.register_keys(pub)
+                t_reg = time.perf_counter() - t_reg
+            d.barrier()
+    else:
+        t_reg = time.perf_counter()
+        valid = ver.register_keys(pub)
+        t_reg = time.perf_counter() - t_reg  # G table + one table per key, built on the device
     assert valid.all()
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
     ver.reserve(n)

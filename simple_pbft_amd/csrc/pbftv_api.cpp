@@ -996,6 +996,64 @@ static int for_each_device(pbftv_ctx* ctx, Fn fn) {
 }
 }  // extern "C++"
 
+// One attempt at a device's tables: geometry from the HBM free now, then the G
+// table (shared per GPU and width) and the key tables (pbftv_register_keys).
+static int register_tables(Device& d, const std::vector<uint32_t>& le, uint32_t k, uint32_t* valid,
+                           std::chrono::steady_clock::time_point t0) {
+  size_t free_b = 0, total_b = 0, held = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  for (auto& b : d.qblocks) held += b->cap;  // the old key tables' HBM counts for the new ones
+  int wg, wq;
+  const int dev_id = d.id;
+  choose_bits(k, free_b + held, &wg, &wq, [&](int g) {
+    std::lock_guard<std::mutex> gl(g_tables_mu);
+    auto it = g_tables.find({dev_id, g});
+    return it != g_tables.end() && !it->second.tab.expired();  // ours or another context's: no new HBM
+  });
+  d.nkeys = 0;
+  if (wq != d.qbits || d.qtab.size() < k) {  // new width or too few slots: new blocks (freeing HBM
+    for (auto& b : d.qblocks) b->release();  // the driver wipes is slow: same-width re-registrations
+    d.qblocks.clear();                       // reuse their slots)
+    d.qtab.clear();
+  }
+  trace("release old key tables", d.id, t0);
+  if (d.gbits != wg || !d.gtab) {  // G table: once per GPU and width while any context holds it
+    d.gtab.reset();
+    d.gbits = 0;
+    std::shared_ptr<std::mutex> build_mu;
+    {
+      std::lock_guard<std::mutex> gl(g_tables_mu);
+      build_mu = g_tables[{d.id, wg}].build;
+    }
+    std::lock_guard<std::mutex> bl(*build_mu);  // one builder per (GPU, width); others wait here, not globally
+    {
+      std::lock_guard<std::mutex> gl(g_tables_mu);
+      d.gtab = g_tables[{d.id, wg}].tab.lock();
+    }
+    if (!d.gtab) {
+      auto t = std::make_shared<DevBuf>();
+      HIP_TRY(t->ensure(pbftv::table_bytes(wg)));
+      DevBuf dummy;
+      HIP_TRY(dummy.ensure(64));
+      trace("G table allocation", d.id, t0);
+      const int r = build_tables(d, wg, nullptr, 0, 1, 1, dummy.as<uint32_t>(), {t->p});
+      if (r != PBFTV_OK) return r;
+      trace("G table build", d.id, t0);
+      {
+        std::lock_guard<std::mutex> gl(g_tables_mu);
+        g_tables[{d.id, wg}].tab = t;
+      }
+      d.gtab = std::move(t);
+    }
+    d.gbits = wg;
+  }
+  d.qbits = wq;
+  const int r = build_key_tables(d, le, 0, k, valid);
+  if (r != PBFTV_OK) return r;
+  d.have_keys = true;
+  return PBFTV_OK;
+}
+
 int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* out_valid) {
   if (!ctx || (k && !pub_xy)) return fail(PBFTV_EINVAL, "null argument");
   const std::vector<uint32_t> le = keys_to_le(pub_xy, k);
@@ -1010,58 +1068,19 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     // stream (pbftv_stream_create + *_dev) may still read the tables, key_valid
     // or qptrs this call rewrites in place
     HIP_TRY(hipDeviceSynchronize());
-    size_t free_b = 0, total_b = 0, held = 0;
-    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    for (auto& b : d.qblocks) held += b->cap;  // the old key tables' HBM counts for the new ones
-    int wg, wq;
-    const int dev_id = d.id;
-    choose_bits(k, free_b + held, &wg, &wq, [&](int g) {
-      std::lock_guard<std::mutex> gl(g_tables_mu);
-      auto it = g_tables.find({dev_id, g});
-      return it != g_tables.end() && !it->second.tab.expired();  // ours or another context's: no new HBM
-    });
-    d.nkeys = 0;
-    if (wq != d.qbits || d.qtab.size() < k) {  // new width or too few slots: new blocks (freeing HBM
-      for (auto& b : d.qblocks) b->release();  // the driver wipes is slow: same-width re-registrations
-      d.qblocks.clear();                       // reuse their slots)
+    // another process or context can take HBM between the free-memory query
+    // and the allocations: on ENOMEM this device's tables are freed and the
+    // geometry is chosen again from what is free then (3 attempts)
+    for (int attempt = 0;; ++attempt) {
+      const int r = register_tables(d, le, k, first ? valid.data() : nullptr, t0);
+      if (r != PBFTV_ENOMEM || attempt == 2) return r;
+      for (auto& b : d.qblocks) b->release();
+      d.qblocks.clear();
       d.qtab.clear();
-    }
-    trace("release old key tables", d.id, t0);
-    if (d.gbits != wg || !d.gtab) {  // G table: once per GPU and width while any context holds it
       d.gtab.reset();
-      d.gbits = 0;
-      std::shared_ptr<std::mutex> build_mu;
-      {
-        std::lock_guard<std::mutex> gl(g_tables_mu);
-        build_mu = g_tables[{d.id, wg}].build;
-      }
-      std::lock_guard<std::mutex> bl(*build_mu);  // one builder per (GPU, width); others wait here, not globally
-      {
-        std::lock_guard<std::mutex> gl(g_tables_mu);
-        d.gtab = g_tables[{d.id, wg}].tab.lock();
-      }
-      if (!d.gtab) {
-        auto t = std::make_shared<DevBuf>();
-        HIP_TRY(t->ensure(pbftv::table_bytes(wg)));
-        DevBuf dummy;
-        HIP_TRY(dummy.ensure(64));
-        trace("G table allocation", d.id, t0);
-        const int r = build_tables(d, wg, nullptr, 0, 1, 1, dummy.as<uint32_t>(), {t->p});
-        if (r != PBFTV_OK) return r;
-        trace("G table build", d.id, t0);
-        {
-          std::lock_guard<std::mutex> gl(g_tables_mu);
-          g_tables[{d.id, wg}].tab = t;
-        }
-        d.gtab = std::move(t);
-      }
-      d.gbits = wg;
+      d.gbits = d.qbits = 0;
+      d.nkeys = 0;
     }
-    d.qbits = wq;
-    const int r = build_key_tables(d, le, 0, k, first ? valid.data() : nullptr);
-    if (r != PBFTV_OK) return r;
-    d.have_keys = true;
-    return PBFTV_OK;
   });
   if (rc != PBFTV_OK) {
     for (auto& dp : ctx->devs) {  // no device keeps a key set the others lack
