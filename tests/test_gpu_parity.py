@@ -132,6 +132,26 @@ def test_sha256_dev_api(ver):
 
 
 # ------------------------------------------------------------------ ECDSA
+def test_ecdsa_empty_batches(ver, ecdsa_fixtures):
+    """n = 0 on every signature entry point: an empty bitmap, no error, no
+    launch; the quorum check counts 0 accepted (quorum 1 fails, quorum 0
+    holds); a following batch is unaffected."""
+    keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
+    ver.register_keys(keys)
+    z32, z64, zk = np.zeros((0, 32), np.uint8), np.zeros((0, 64), np.uint8), np.zeros(0, np.uint32)
+    assert ver.verify_batch(z32, z64, zk).shape == (0,)
+    bm, acc, ok = ver.qc_verify(z32, z64, zk, quorum=1)
+    assert bm.shape == (0,) and acc == 0 and not ok
+    assert ver.qc_verify(z32, z64, zk, quorum=0)[2]
+    d = ver.alloc(0, 64)
+    try:
+        ver.verify_batch_dev(0, d.ptr, d.ptr, d.ptr, 0, d.ptr)
+        ver.sync(0)
+    finally:
+        d.free()
+    assert (ver.verify_batch(hashes, sigs, kidx) == expect).all()
+
+
 def test_register_keys_validity(ver, ecdsa_fixtures):
     keys, *_ = fixture_arrays(ecdsa_fixtures)
     valid = ver.register_keys(keys)
