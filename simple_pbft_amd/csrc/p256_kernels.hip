@@ -470,10 +470,12 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
   __shared__ uint32_t spre[kPrefixLds ? (K > 1 ? K - 1 : 1) : 1][9][256];
   const bool sorted = ko.total != nullptr;  // block-uniform
   const uint32_t nk = ko.nkeys;
+  PBFTV_SPROBE(0, nk);
   if (sorted) {
     for (uint32_t b = threadIdx.x; b <= nk; b += blockDim.x) kh[b] = 0;
     block_key_starts(ko.total, nk, kstart, kpart);  // (ends with a barrier: kh[] is clear)
   }
+  PBFTV_SPROBE(1, kstart[0]);
   // The forward pass reads s only (32 B): an s outside (0, n) joins the
   // products as 1.  r, the key and the hash are read once, in the backward
   // pass, where Go's remaining checks decide the record's ok.
@@ -524,6 +526,7 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
     }
     okm |= (oks ? 1u : 0u) << j;
   }
+  PBFTV_SPROBE(2, acc.v[0]);
   fe_set(rk, kRPowN[K + 1]);
   fn_mul(acc, acc, rk);        // P R: the lane total in Montgomery form
   if (sorted) {  // claim this block's range of every key: kh[] becomes its cursors
@@ -532,6 +535,7 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
       if (kh[b]) kh[b] = kstart[b] + atomicAdd(&ko.claim[b], kh[b]);
     __syncthreads();
   }
+  PBFTV_SPROBE(3, acc.v[0]);
   fe inv;
   if constexpr (K >= PBFTV_SCAL_BLOCK_INV_MIN_K) {
     // P^-1 R: one inversion and one cross-lane scan per 256-thread block, 6
@@ -545,6 +549,7 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
   } else {
     wave_batch_inv_n(inv, acc);  // P^-1 R: one inversion per wave (64 K signatures)
   }
+  PBFTV_SPROBE(4, inv.v[0]);
   if (K > 1) {
     fe_set(rk, kRPowN[K]);
     fn_mul(inv, inv, rk);      // P^-1 R^K
@@ -618,6 +623,7 @@ __global__ void __launch_bounds__(256, PBFTV_SCAL_WAVES) k_ecdsa_scalars(const u
       o->q[6] = make_uint4(ok ? kj : 0u, (uint32_t)i, ok ? 1u : 0u, 0u);
     }
   }
+  PBFTV_SPROBE(5, okm);
 }
 
 // LSB-first bitmap from one byte per signature
@@ -769,3 +775,10 @@ hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const 
 size_t ecdsa_record_bytes(uint64_t n) { return (size_t)n * sizeof(SigRec); }
 
 }  // namespace pbftv
+
+#ifdef PBFTV_SCAL_PROBE
+extern "C" int pbftv_debug_scal_probe(uint64_t* out, size_t n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(pbftv::g_scal_probe), n * sizeof(uint64_t), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

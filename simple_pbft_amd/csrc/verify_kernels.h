@@ -26,6 +26,26 @@ namespace pbftv {
 #define PBFTV_COMB_WAVES 4  // min waves per SIMD for k_ecdsa_comb: 128 VGPRs; +1.2 % over 2 (tools/ab.sh)
 #endif
 
+// Stage timing probe (experiment builds only: make EXTRA=-DPBFTV_SCAL_PROBE,
+// read by tools/scal_probe.py): lane 0 of each wave stamps wall_clock64() at
+// the stage boundaries of k_ecdsa_scalars (slots 0..5) and of
+// wave_batch_inv_n (6: scans, 7: safegcd); the asm ties a stamp to the value
+// the stage produced.
+#ifdef PBFTV_SCAL_PROBE
+static __device__ uint64_t g_scal_probe[8192 * 8];
+#define PBFTV_SPROBE(k, dep)                                                            \
+  do {                                                                                  \
+    asm volatile("" ::"v"(dep));                                                        \
+    const uint64_t t_ = wall_clock64();                                                 \
+    const uint64_t w_ = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;         \
+    if ((threadIdx.x & 63u) == 0 && w_ < 8192) g_scal_probe[w_ * 8 + (k)] = t_;         \
+  } while (0)
+#else
+#define PBFTV_SPROBE(k, dep) \
+  do {                       \
+  } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // 32 big-endian bytes at p (16-B aligned) -> 8 LE words
@@ -916,6 +936,7 @@ __device__ __forceinline__ void wave_batch_inv_n(fe& inv, const fe& acc) {
     fn_mul(pre, pre, a);  // inclusive prefix product
     fn_mul(suf, suf, b);  // inclusive suffix product
   }
+  PBFTV_SPROBE(6, suf.v[0] ^ pre.v[0]);
   fe tot;
   fn_canon(tot, pre);
   uint32_t w[8];
@@ -923,6 +944,7 @@ __device__ __forceinline__ void wave_batch_inv_n(fe& inv, const fe& acc) {
   PBFTV_UNROLL for (int k = 0; k < 8; ++k) w[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 63);
   fe D, r2n, invt;
   inv_mod_n_wave(D, w);  // R / total: the plain inverse of the product of the (plain) values
+  PBFTV_SPROBE(7, D.v[0]);
   fe_set(r2n, kR2N);
   fn_mul(invt, D, r2n);  // its Montgomery form
   shfl_fe(a, pre, lane - 1);
