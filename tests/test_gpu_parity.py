@@ -470,9 +470,9 @@ def test_dev_calls_on_two_streams_share_scratch(ver, oracle_lib, monkeypatch):
 def test_armed_path_golden_and_crafted(ecdsa_fixtures):
     """Every golden vector (valid, high-S, the corruption classes, e >= n,
     R.x >= n, invalid keys, the crafted doubling / cancellation sums) and the
-    chosen-scalar exceptional sums, served in calls of 1-8 signatures -- the
-    sizes the armed kernel takes from its mailbox slots -- against the
-    fixtures' expected bits."""
+    chosen-scalar exceptional sums, served in calls of 1-8 signatures (the
+    armed kernel's mailbox slots) and of 9-128 (one launch of the latency
+    kernel reading the mailbox arrays) -- against the fixtures' expected bits."""
     from conftest import crafted_exceptional
     from simple_pbft_amd import Verifier
     keys, hashes, sigs, kidx, expect = fixture_arrays(ecdsa_fixtures)
@@ -482,7 +482,7 @@ def test_armed_path_golden_and_crafted(ecdsa_fixtures):
         o = rng.permutation(len(kidx))
         at = 0
         while at < len(o):
-            m = int(rng.integers(1, 9))
+            m = int(rng.choice([1, 2, 3, 5, 8, 9, 13, 24, 67, 128]))
             sel = o[at:at + m]
             got = v.verify_batch(hashes[sel], sigs[sel], kidx[sel])
             bad = [ecdsa_fixtures["vectors"][i]["kind"] for i, g in zip(sel, got) if g != expect[i]]
@@ -492,6 +492,7 @@ def test_armed_path_golden_and_crafted(ecdsa_fixtures):
         v.register_keys(key)
         for a in range(0, len(K), 4):
             assert (v.verify_batch(H[a:a + 4], S[a:a + 4], K[a:a + 4]) == E[a:a + 4]).all(), a
+        assert (v.verify_batch(H, S, K) == E).all()  # all of them in one call (past the slots when > 8)
 
 
 
