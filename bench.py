@@ -186,25 +186,71 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int):
-    """p50 / p99 of pbftv_qc_verify on one certificate from host buffers, called
-    with pre-marshalled ctypes arguments (one foreign call per certificate, as a
-    cgo caller would make it).  Every call verifies a DIFFERENT certificate, so
-    its table entries come cold from HBM as they would for fresh votes."""
-    warm = 20
-    pub, H, S, K = synth.certs(n_keys, sigs, iters + warm, seed)
-    ver.register_keys(pub)
-    calls = [ver.qc_verify_prepared(H[c * sigs:(c + 1) * sigs], S[c * sigs:(c + 1) * sigs],
-                                    K[c * sigs:(c + 1) * sigs], quorum=sigs) for c in range(iters + warm)]
-    for c in range(warm):
-        calls[c]()
-    ts = []
-    for call in calls[warm:]:
-        t0 = time.perf_counter()
-        acc, ok = call()
-        ts.append(time.perf_counter() - t0)
-        assert ok and acc == sigs
-    return float(np.percentile(ts, 50) * 1e6), float(np.percentile(ts, 99) * 1e6)
+_QC_DRIVER = None
+
+
+def qc_driver():
+    """tools/qc_driver.c (built by __graft_entry__.build()): the per-certificate
+    caller loop in C, calling pbftv_qc_verify through its function pointer."""
+    global _QC_DRIVER
+    if _QC_DRIVER is None:
+        L = ctypes.CDLL(os.path.join(ROOT, "tools", "libqc_driver.so"))
+        vp = ctypes.c_void_p
+        L.qc_drive.restype = ctypes.c_int
+        L.qc_drive.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                               ctypes.c_double, vp, vp, vp]
+        _QC_DRIVER = L
+    return _QC_DRIVER
+
+
+def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int, gap_s: float = 0.0, warm: int = 20,
+               register: bool = True, certs=None):
+    """Latency of pbftv_qc_verify on one certificate from host buffers: every
+    call verifies a DIFFERENT certificate (its table entries come cold from HBM,
+    as for fresh votes), made from C (tools/qc_driver.c: nanosleep(gap) before
+    each call, CLOCK_MONOTONIC around it) as a compiled cgo caller would make
+    it.  gap_s = 1.0 is the reference's cadence: one flush per 1-s alarm
+    (pbft/network/node.go:44, :513-518).  Returns p50 / p90 / p99 / min in us
+    and the medians of the library's own diagnostics (pbftv_qc_stamps): host
+    time inside the call, and for armed serves the GPU's serve time and clock."""
+    if certs is None:
+        pub, H, S, K = synth.certs(n_keys, sigs, iters + warm, seed)
+        if register:
+            ver.register_keys(pub)
+    else:
+        H, S, K = certs
+    H, S, K = (np.ascontiguousarray(a) for a in (H, S, K))
+    L = lib_handle(ver)
+    fn = ctypes.cast(L.pbftv_qc_verify, ctypes.c_void_p).value
+    st = ctypes.cast(L.pbftv_qc_stamps, ctypes.c_void_p).value
+    D = qc_driver()
+
+    def drive(lo, cnt, gap):
+        us = np.zeros(cnt)
+        acc = np.zeros(cnt, np.uint64)
+        stamps = np.zeros((cnt, 8), np.uint64)
+        bad = D.qc_drive(fn, st, ver.handle.value, H[lo * sigs:].ctypes.data, S[lo * sigs:].ctypes.data,
+                         K[lo * sigs:].ctypes.data, cnt, sigs, sigs, gap * 1e6, us.ctypes.data, acc.ctypes.data,
+                         stamps.ctypes.data)
+        assert bad == 0 and (acc == sigs).all(), (bad, acc[acc != sigs][:4])
+        return us, stamps
+    drive(0, warm, 0.0)
+    us, stamps = drive(warm, iters, gap_s)
+    out = {"p50": float(np.percentile(us, 50)), "p90": float(np.percentile(us, 90)),
+           "p99": float(np.percentile(us, 99)), "min": float(us.min()), "calls": iters, "gap_s": gap_s}
+    out["in_library_us_p50"] = float(np.median(stamps[:, 1])) * 1e-3
+    armed = stamps[:, 2] == 1
+    out["armed_frac"] = float(armed.mean())
+    if armed.any():
+        a = stamps[armed].astype(np.float64)
+        wall = (a[:, 5] - a[:, 3]) / (a[:, 7] * 1e3)
+        out["gpu_serve_us_p50"] = float(np.median(wall)) * 1e6
+        out["gpu_sclk_mhz_p50"] = float(np.median((a[:, 6] - a[:, 4]) / np.maximum(wall, 1e-9))) * 1e-6
+    return out
+
+
+def lib_handle(ver: Verifier):
+    return ver._L
 
 
 def cpu_model() -> str:

@@ -108,6 +108,14 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
 int pbftv_set_kernel_timing(pbftv_ctx* ctx, int enable);
 int pbftv_kernel_time_ms(pbftv_ctx* ctx, int dev, int kernel, double* out_ms, uint64_t* out_launches);
 int pbftv_reset_kernel_times(pbftv_ctx* ctx);
+/* Diagnostics of the last latency-path call (n <= 2048) on device dev:
+ * out[0] = host ns from entry to the request being handed over (bell rung or
+ * kernel launched), out[1] = host ns from entry to return, out[2] = 1 if an
+ * armed kernel served it, 0 if a launch did, out[3..6] = the armed kernel's
+ * slot-0 wave: GPU wall clock and shader clock when it saw the request, and
+ * when it wrote its verdict (0 after a launch), out[7] = the wall-clock rate
+ * in kHz. */
+int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]);
 
 /* ---- SHA-256 digests (utils.Hash) ------------------------------------ */
 

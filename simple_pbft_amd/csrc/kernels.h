@@ -112,13 +112,16 @@ uint64_t wave_path_max();
 // indices cap*4) and one result byte per signature.  The host writes the
 // inputs, n and then bell = the request's sequence number; an armed kernel
 // (k_ecdsa_wave_armed) waiting for that number serves it; stop = seq cancels
-// the armed kernel, which then reports expired = seq (verify_kernels.h).
+// the armed kernel, which then reports expired = seq (verify_kernels.h); so
+// does any change of halt (a disarm, or the process-wide quiesce of a GPU,
+// pbftv_api.cpp).  live = the first request number of the newest armed kernel
+// that has started (written by it: a rotation retires the old one after that).
 // The first kQcSlots signatures are also written to their own 3-line slot
 // (slot_off): line 0 = {tag, n, key, 0, hash[32], 0, 0, 0, tag}, line 1 =
 // {tag, 0, 0, 0, r[32], 0, 0, 0, tag}, line 2 likewise with s; the tags (the
 // request number) are written after their line's data, the last dword first.
 struct QcMail {
-  uint32_t bell, n, stop, expired, cap, pad[11];
+  uint32_t bell, n, stop, expired, cap, halt, live, pad[9];
   static constexpr uint32_t kQcSlots = 8;
   static constexpr size_t slot_off(uint32_t i) { return 64 + 192 * (size_t)i; }
   static constexpr size_t arrays_off() { return 64 + 192 * (size_t)kQcSlots; }
@@ -126,7 +129,10 @@ struct QcMail {
   static constexpr size_t sigs_off(uint32_t cap) { return arrays_off() + 32 * (size_t)cap; }
   static constexpr size_t keys_off(uint32_t cap) { return arrays_off() + 96 * (size_t)cap; }
   static constexpr size_t res_off(uint32_t cap) { return arrays_off() + 100 * (size_t)cap; }
-  static constexpr size_t bytes(uint32_t cap) { return arrays_off() + 101 * (size_t)cap + 64; }
+  // diagnostics: per slot, the armed wave's {wall clock, shader clock} when it
+  // saw its request and when it wrote its verdict (pbftv_qc_stamps)
+  static constexpr size_t stamps_off(uint32_t cap) { return (res_off(cap) + cap + 63) & ~(size_t)63; }
+  static constexpr size_t bytes(uint32_t cap) { return stamps_off(cap) + 32 * (size_t)kQcSlots + 64; }
 };
 struct ArmArgs {
   QcMail* mail;
@@ -136,6 +142,8 @@ struct ArmArgs {
   uint32_t nkeys;
   const uint32_t* gtab;
   const uint32_t* const* qtabs;
+  uint32_t spin;       // between polls: 0 = s_sleep, 1 = none, k >= 2 = k dependent VALU ops
+  uint32_t halt;       // the mailbox's halt word at arming: any other value cancels
 };
 hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st);
 

@@ -54,13 +54,68 @@ int fail(int code, const std::string& msg) {
                   std::string(#expr) + ": " + hipGetErrorString(e_));                                         \
   } while (0)
 
-// grow-only device buffer
+// ---- armed latency kernels, process-wide (k_ecdsa_wave_armed) ----
+// An armed kernel stays resident on its GPU between latency-path calls, and
+// hipFree / hipHostFree / hipDeviceSynchronize wait for every kernel on the
+// GPU.  So every library path that frees memory or synchronises a whole device
+// first QUIESCES that GPU: it bumps the `halt` word of every registered mailbox
+// on it (each armed kernel was launched with the value it then held and leaves
+// within one poll of a change, reporting `expired`, which sends its owner's
+// next call through a launch), and no context arms a kernel on that GPU until
+// the quiesce ends.  Other contexts' kernels are cancelled without their locks:
+// the mailbox words are host memory and the halt bump is one atomic add.
+struct ArmRegistry {
+  std::mutex mu;
+  std::map<int, std::vector<pbftv::QcMail*>> mail;  // GPU -> registered mailboxes
+  std::map<int, int> quiesce;                       // GPU -> quiesces in progress
+};
+ArmRegistry& arm_registry() {
+  static ArmRegistry* r = new ArmRegistry;  // never destroyed: DevBuf destructors may run at exit
+  return *r;
+}
+
+// gpu < 0: every GPU (a pinned host buffer is not tied to one device)
+void halt_armed_locked(ArmRegistry& r, int gpu) {
+  for (auto& kv : r.mail)
+    if (gpu < 0 || kv.first == gpu)
+      for (pbftv::QcMail* m : kv.second) __atomic_add_fetch(&m->halt, 1u, __ATOMIC_RELEASE);
+}
+
+bool arming_allowed_locked(ArmRegistry& r, int gpu) { return r.quiesce[gpu] == 0 && r.quiesce[-1] == 0; }
+
+struct GpuQuiesce {
+  int gpu;  // < 0: all
+  explicit GpuQuiesce(int g) : gpu(g) {
+    ArmRegistry& r = arm_registry();
+    std::lock_guard<std::mutex> lk(r.mu);
+    ++r.quiesce[gpu];
+    halt_armed_locked(r, gpu);
+  }
+  ~GpuQuiesce() {
+    ArmRegistry& r = arm_registry();
+    std::lock_guard<std::mutex> lk(r.mu);
+    --r.quiesce[gpu];
+  }
+  GpuQuiesce(const GpuQuiesce&) = delete;
+  GpuQuiesce& operator=(const GpuQuiesce&) = delete;
+};
+
+int current_gpu() {
+  int g = 0;
+  (void)hipGetDevice(&g);
+  return g;
+}
+
+// grow-only device buffer (a free quiesces the current GPU first)
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
+    if (p) {
+      GpuQuiesce q(current_gpu());
+      (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 4096);
@@ -69,7 +124,10 @@ struct DevBuf {
     return e;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      GpuQuiesce q(current_gpu());
+      (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
   }
@@ -91,7 +149,10 @@ struct HostBuf {
   unsigned flags = hipHostMallocCoherent | hipHostMallocMapped;  // plain pinned (DMA staging): hipHostMallocDefault
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      GpuQuiesce q(-1);
+      (void)hipHostFree(p);
+    }
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 1 << 16);
@@ -100,7 +161,10 @@ struct HostBuf {
     return e;
   }
   void release() {
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      GpuQuiesce q(-1);
+      (void)hipHostFree(p);
+    }
     p = nullptr;
     cap = 0;
   }
@@ -147,11 +211,23 @@ struct Device {
   DevBuf hashes, sigs, key_idx, bitmap;
   VerifyScratch vs;  // the lane path's stage-1 records, prefix products, key order, result bytes
   HostBuf stage;  // zero-copy inputs/outputs of the small-batch path (a QcMail mailbox)
-  // the armed latency kernel (k_ecdsa_wave_armed): launched after every
-  // latency-path call, it waits for the next request's doorbell in `stage`;
-  // arm_seq = the request number it waits for (0: none armed)
-  hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: the next kernel spins while this one works
-  uint32_t arm_seq = 0, seq_counter = 0;
+  // the armed latency kernel (k_ecdsa_wave_armed): a persistent server that
+  // waits for the next request's doorbell in `stage`; arm_seq = the request
+  // number it waits for (0: none armed)
+  hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: a rotation's successor spins beside its predecessor
+  uint32_t arm_seq = 0, seq_counter = 0;  // (the armed kernel serves arm_seq, arm_seq + 1, ...)
+  int arm_stream = 1;                      // qstream index of the armed kernel
+  uint32_t armed_first = 0;                // the armed kernel's first number (its `live` report)
+  uint32_t retiring = 0;                   // a rotated-out kernel still waiting for arm_seq's to start
+  bool mail_registered = false;  // the mailbox is in the arm registry
+  std::chrono::steady_clock::time_point armed_at{}, last_qc{};
+  std::thread keeper;  // qc_keeper_loop
+  std::condition_variable keeper_cv;
+  bool keeper_stop = false, keeper_idle = false;
+  uint64_t rotations = 0;
+  // diagnostics of the last latency-path call (pbftv_qc_stamps)
+  uint64_t qc_ns_handover = 0, qc_ns_total = 0;
+  bool qc_armed_served = false;
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
   static constexpr int kSlots = 16;  // chunks staged ahead at most (PBFTV_HOST_SLOTS, default 16)
@@ -273,49 +349,178 @@ bool qc_arm_enabled() {
   return e ? e[0] == '1' : true;
 }
 
-// wall-clock ticks the armed kernel waits for its request (PBFTV_QC_ARM_MS, default 500 ms)
-uint64_t qc_arm_budget() {
-  static const uint64_t ticks = [] {
-    double ms = 500.0;
-    if (const char* e = getenv("PBFTV_QC_ARM_MS")) ms = atof(e);
-    int khz = 100000;
-    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
-    return (uint64_t)(ms * khz);
-  }();
-  return ticks;
+double env_ms(const char* name, double dflt) {
+  const char* e = getenv(name);
+  return e ? atof(e) : dflt;
+}
+
+// How long one armed kernel waits for its request (PBFTV_QC_ARM_MS, default
+// 100 ms; read at every arming), in wall-clock ticks of device dev.  A context
+// that keeps making latency-path calls never sees a kernel run out: its keeper
+// thread replaces the armed kernel at half its budget (qc_keeper_loop) for as
+// long as the last call is less than PBFTV_QC_KEEP_MS (default 10 s) ago, so
+// the reference's 1-s alarm cadence (pbft/network/node.go:44) finds one waiting.
+// The budget bounds how long a hipDeviceSynchronize / hipFree made OUTSIDE the
+// library on that GPU can wait for an armed kernel (~1.5 budgets).
+double qc_arm_ms() { return env_ms("PBFTV_QC_ARM_MS", 100.0); }
+double qc_keep_ms() { return env_ms("PBFTV_QC_KEEP_MS", 10000.0); }
+
+uint64_t qc_arm_budget(int dev) {
+  int khz = 100000;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  return (uint64_t)(qc_arm_ms() * khz);
+}
+
+// what the armed kernel does between polls (ArmArgs::spin; PBFTV_QC_SPIN)
+uint32_t qc_spin() {
+  const char* e = getenv("PBFTV_QC_SPIN");
+  return e ? (uint32_t)atoi(e) : 0u;
 }
 
 QcMail* qc_mail(Device& d) { return d.stage.as<QcMail>(); }
 
-hipError_t qc_mail_ready(Device& d) {
-  if (d.stage.cap >= QcMail::bytes(kQcCap)) return hipSuccess;
-  HIP_TRY_E(d.stage.ensure(QcMail::bytes(kQcCap)));
-  std::memset(d.stage.p, 0, QcMail::bytes(kQcCap));
-  qc_mail(d)->cap = kQcCap;
+// the mailbox enters the process-wide registry (so a quiesce of its GPU halts
+// its kernels) and leaves it before its memory is released
+void qc_register(Device& d) {
+  if (d.mail_registered || !d.stage.p) return;
+  ArmRegistry& r = arm_registry();
+  std::lock_guard<std::mutex> lk(r.mu);
+  r.mail[d.id].push_back(qc_mail(d));
+  d.mail_registered = true;
+}
+
+void qc_unregister(Device& d) {
+  if (!d.mail_registered) return;
+  ArmRegistry& r = arm_registry();
+  std::lock_guard<std::mutex> lk(r.mu);
+  auto& v = r.mail[d.id];
+  v.erase(std::remove(v.begin(), v.end(), qc_mail(d)), v.end());
+  d.mail_registered = false;
+}
+
+// (re)lay out the mailbox for up to cap signatures
+hipError_t qc_mail_layout(Device& d, uint32_t cap) {
+  if (d.stage.cap < QcMail::bytes(cap)) {
+    qc_unregister(d);
+    HIP_TRY_E(d.stage.ensure(QcMail::bytes(cap)));
+  }
+  std::memset(d.stage.p, 0, QcMail::bytes(cap));
+  qc_mail(d)->cap = cap;
+  qc_register(d);
   return hipSuccess;
 }
 
-// Cancel the armed kernel (if any) and wait until every armed kernel has exited.
+hipError_t qc_mail_ready(Device& d) {
+  if (d.stage.p && d.mail_registered) return hipSuccess;
+  return qc_mail_layout(d, kQcCap);
+}
+
+// Cancel the armed kernels of this device (halt bump) and wait until they have exited.
 hipError_t qc_disarm(Device& d) {
-  if (d.arm_seq) __atomic_store_n(&qc_mail(d)->stop, d.arm_seq, __ATOMIC_RELEASE);
+  if (d.stage.p && d.mail_registered) __atomic_add_fetch(&qc_mail(d)->halt, 1u, __ATOMIC_RELEASE);
   d.arm_seq = 0;
+  d.retiring = 0;
   for (hipStream_t q : d.qstream)
     if (q) HIP_TRY_E(hipStreamSynchronize(q));
   return hipSuccess;
 }
 
-// Launch the kernel that will serve the next latency-path request.
+void qc_keeper_loop(Device* d);
+
+// Launch the kernel that will serve the next latency-path request (none while
+// a quiesce of this GPU is in progress: the request then takes a launch).
 hipError_t qc_arm(Device& d) {
   if (d.arm_seq || !qc_arm_enabled() || !d.have_keys) return hipSuccess;
   HIP_TRY_E(qc_mail_ready(d));
   for (hipStream_t& q : d.qstream)
     if (!q) HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-  const uint32_t want = ++d.seq_counter, slot = want & 1u;
-  const ArmArgs a{qc_mail(d), want, qc_arm_budget(), d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
-                  d.qptrs.as<const uint32_t* const>()};
+  uint32_t halt;
+  {
+    // the check and the halt snapshot in one critical section: a quiesce that
+    // starts after it bumps halt, and the new kernel leaves at its first poll
+    ArmRegistry& r = arm_registry();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!arming_allowed_locked(r, d.id)) return hipSuccess;
+    halt = __atomic_load_n(&qc_mail(d)->halt, __ATOMIC_ACQUIRE);
+  }
+  if (++d.seq_counter == 0) d.seq_counter = 1;  // 0 means "none armed"
+  const uint32_t want = d.seq_counter;
+  const int slot = d.arm_stream ^ 1;  // not behind the previous armed kernel (a rotation overlaps the two)
+  const ArmArgs a{qc_mail(d), want, qc_arm_budget(d.id), d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
+                  d.qptrs.as<const uint32_t* const>(), qc_spin(), halt};
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
-  d.arm_seq = want;
+  d.arm_seq = d.armed_first = want;
+  d.arm_stream = slot;
+  d.armed_at = std::chrono::steady_clock::now();
+  if (!d.keeper.joinable() && qc_keep_ms() > 0) d.keeper = std::thread(qc_keeper_loop, &d);
+  d.keeper_cv.notify_one();
   return hipSuccess;
+}
+
+// Replace the armed kernel before it runs out: the successor is launched on
+// the other stream; the old one keeps serving nothing but stays resident until
+// the successor reports itself live (its waves may wait for free slots behind
+// a large batch), then the keeper retires it (stop = its number).  No request
+// is in flight meanwhile: both run under d.mu.
+hipError_t qc_rotate(Device& d) {
+  const uint32_t old = d.arm_seq;
+  d.arm_seq = 0;
+  hipError_t e = qc_arm(d);
+  if (e != hipSuccess || d.arm_seq == 0) {  // not now (quiesce): the old one runs out
+    d.arm_seq = old;
+    return e;
+  }
+  if (old) {
+    if (d.retiring) __atomic_store_n(&qc_mail(d)->stop, d.retiring, __ATOMIC_RELEASE);  // (not live yet: rare)
+    d.retiring = old;
+  }
+  return hipSuccess;
+}
+
+// retire the rotated-out kernel once its successor is resident
+void qc_retire(Device& d) {
+  if (!d.retiring || !d.arm_seq) return;
+  if (__atomic_load_n(&qc_mail(d)->live, __ATOMIC_ACQUIRE) != d.armed_first) return;
+  __atomic_store_n(&qc_mail(d)->stop, d.retiring, __ATOMIC_RELEASE);
+  d.retiring = 0;
+}
+
+// One per device with a latency path in use: keeps an armed kernel waiting
+// while calls keep coming (PBFTV_QC_KEEP_MS after the last one), so a call
+// after an idle gap longer than the budget still finds one.
+void qc_keeper_loop(Device* d) {
+  std::unique_lock<std::mutex> lk(d->mu);
+  (void)hipSetDevice(d->id);
+  const auto far = std::chrono::hours(1);
+  while (!d->keeper_stop) {
+    const auto now = std::chrono::steady_clock::now();
+    const auto half = std::chrono::microseconds((int64_t)(qc_arm_ms() * 500.0));
+    const auto keep = std::chrono::microseconds((int64_t)(qc_keep_ms() * 1000.0));
+    auto wake = now + far;
+    qc_retire(*d);
+    if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
+      // also re-arms after a disarm (key change) or a halt (quiesce)
+      if (d->arm_seq == 0 || now >= d->armed_at + half) {
+        if (qc_rotate(*d) != hipSuccess) (void)hipGetLastError();  // a call will launch instead
+        ++d->rotations;
+      }
+      wake = d->arm_seq ? std::min(d->armed_at + half, d->last_qc + keep) : now + std::chrono::milliseconds(1);
+    }
+    if (d->retiring) wake = std::min(wake, now + std::chrono::milliseconds(1));
+    if (wake <= now) wake = now + std::chrono::milliseconds(1);
+    d->keeper_idle = wake - now > std::chrono::minutes(1);  // a call wakes it (d.last_qc moved)
+    d->keeper_cv.wait_until(lk, wake);
+  }
+}
+
+// stop the keeper (not under d.mu)
+void qc_keeper_stop(Device& d) {
+  {
+    std::lock_guard<std::mutex> lk(d.mu);
+    d.keeper_stop = true;
+  }
+  d.keeper_cv.notify_one();
+  if (d.keeper.joinable()) d.keeper.join();
 }
 
 }  // namespace
@@ -586,10 +791,12 @@ int pbftv_open(pbftv_ctx** out, uint32_t device_mask) {
 
 void pbftv_close(pbftv_ctx* ctx) {
   if (!ctx) return;
+  for (auto& d : ctx->devs) qc_keeper_stop(*d);
   for (auto& d : ctx->devs) {
     std::lock_guard<std::mutex> lk(d->mu);
     (void)hipSetDevice(d->id);
     (void)qc_disarm(*d);  // the armed latency kernels exit before anything is freed
+    qc_unregister(*d);
     for (hipStream_t q : d->qstream)
       if (q) (void)hipStreamDestroy(q);
     (void)hipStreamSynchronize(d->stream);
@@ -676,7 +883,10 @@ int pbftv_host_alloc(pbftv_ctx* ctx, uint64_t bytes, void** out_ptr) {
 
 int pbftv_host_free(pbftv_ctx* ctx, void* ptr) {
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
-  if (ptr) HIP_TRY(hipHostFree(ptr));
+  if (ptr) {
+    GpuQuiesce quiet(-1);  // hipHostFree waits for every kernel: armed ones leave first
+    HIP_TRY(hipHostFree(ptr));
+  }
   return PBFTV_OK;
 }
 
@@ -684,7 +894,10 @@ int pbftv_dev_free(pbftv_ctx* ctx, int dev, void* ptr) {
   Device* d = dev_of(ctx, dev);
   if (!d) return fail(PBFTV_EINVAL, "bad context or device index");
   HIP_TRY(hipSetDevice(d->id));
-  if (ptr) HIP_TRY(hipFree(ptr));
+  if (ptr) {
+    GpuQuiesce quiet(d->id);  // hipFree waits for every kernel on the GPU: armed ones leave first
+    HIP_TRY(hipFree(ptr));
+  }
   return PBFTV_OK;
 }
 
@@ -1062,7 +1275,10 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
     auto t0 = std::chrono::steady_clock::now();
-    HIP_TRY(qc_disarm(d));  // the armed latency kernel reads the tables too (and would hold the sync)
+    // every armed latency kernel on this GPU leaves first (this context's reads
+    // the tables; any context's would hold the device synchronisation below)
+    GpuQuiesce quiet(d.id);
+    HIP_TRY(qc_disarm(d));
     d.have_keys = false;
     // every stream of the GPU, not only ours: a verify enqueued on a caller
     // stream (pbftv_stream_create + *_dev) may still read the tables, key_valid
@@ -1102,6 +1318,7 @@ int pbftv_add_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* o
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
+    GpuQuiesce quiet(d.id);  // (as in pbftv_register_keys)
     HIP_TRY(qc_disarm(d));
     HIP_TRY(hipDeviceSynchronize());  // caller streams too: qptrs and key_valid are rewritten
     return build_key_tables(d, le, d.nkeys, k, first ? valid.data() : nullptr);
@@ -1130,6 +1347,7 @@ int pbftv_set_key(pbftv_ctx* ctx, uint32_t index, const uint8_t* pub_xy, uint8_t
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
+    GpuQuiesce quiet(d.id);  // (as in pbftv_register_keys)
     HIP_TRY(qc_disarm(d));
     HIP_TRY(hipDeviceSynchronize());  // no verify on any stream (caller streams too) still reads the old table
     return build_key_tables(d, le, index, 1, first ? &valid : nullptr);
@@ -1322,37 +1540,44 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     // latency path on the first device: inputs packed into pinned coherent
     // host memory (the QcMail mailbox) that the kernel reads directly, one byte
     // per signature written back the same way and polled for (sentinel 0xFF):
-    // no copies, no stream synchronisation on the fast path.  Up to kQcCap
-    // signatures are served by the ARMED kernel launched at the end of the
-    // previous call (k_ecdsa_wave_armed: the request rings its doorbell, no
-    // launch on the critical path); otherwise, or when it expired, one launch of
-    // k_ecdsa_wave.  The next armed kernel is launched while this request
-    // computes, on the other of two streams, so it is already spinning when a
-    // back-to-back request rings.
+    // no copies, no stream synchronisation on the fast path.  Up to kQcSlots
+    // signatures (a certificate of n <= 9 replicas) are served by the ARMED
+    // kernel (k_ecdsa_wave_armed), a persistent server kept waiting on this
+    // device (qc_arm, qc_keeper_loop): the request writes its slot lines and
+    // rings, and nothing else -- no launch, no HIP call -- is on its path.
+    // Otherwise, or when the armed kernel has run out, one launch of
+    // k_ecdsa_wave (up to 2048 signatures, one wave each).
     Device& d = *ctx->devs[0];
     std::lock_guard<std::mutex> lk(d.mu);
-    HIP_TRY(hipSetDevice(d.id));
+    const auto h_in = std::chrono::steady_clock::now();
+    d.last_qc = h_in;
+    bool dev_set = false;
+    auto set_dev = [&]() -> hipError_t {  // only paths that make HIP calls pay for it
+      if (dev_set) return hipSuccess;
+      dev_set = true;
+      return hipSetDevice(d.id);
+    };
     const bool small = n <= kQcCap;
-    if (!small) HIP_TRY(qc_disarm(d));  // (the mailbox is relaid out for n)
     const uint32_t cap = small ? kQcCap : (uint32_t)n;
-    if (d.stage.cap < QcMail::bytes(cap)) {
-      HIP_TRY(qc_disarm(d));
-      HIP_TRY(d.stage.ensure(QcMail::bytes(cap)));
-      std::memset(d.stage.p, 0, QcMail::bytes(cap));
+    if (!small || d.stage.cap < QcMail::bytes(cap) || !d.mail_registered) {
+      HIP_TRY(set_dev());
+      HIP_TRY(qc_disarm(d));  // (the mailbox is relaid out for n)
+      HIP_TRY(qc_mail_layout(d, cap));
     }
     QcMail* m = qc_mail(d);
     uint8_t* st8 = d.stage.as<uint8_t>();
-    uint8_t* const hp = st8 + QcMail::hashes_off();
-    uint8_t* const sp = st8 + QcMail::sigs_off(cap);
-    uint32_t* const kp = reinterpret_cast<uint32_t*>(st8 + QcMail::keys_off(cap));
     volatile uint8_t* const res = st8 + QcMail::res_off(cap);
-    std::memcpy(hp, hashes, 32 * n);
-    std::memcpy(sp, sig_rs, 64 * n);
-    std::memcpy(kp, key_idx, 4 * n);
     std::memset(const_cast<uint8_t*>(res), 0xFF, n);
     m->cap = cap;
     m->n = (uint32_t)n;
     auto launch_plain = [&]() -> int {
+      uint8_t* const hp = st8 + QcMail::hashes_off();
+      uint8_t* const sp = st8 + QcMail::sigs_off(cap);
+      uint32_t* const kp = reinterpret_cast<uint32_t*>(st8 + QcMail::keys_off(cap));
+      std::memcpy(hp, hashes, 32 * n);
+      std::memcpy(sp, sig_rs, 64 * n);
+      std::memcpy(kp, key_idx, 4 * n);
+      HIP_TRY(set_dev());
       HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
         return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n, d.key_valid.as<uint32_t>(), d.nkeys,
                                         d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,
@@ -1360,13 +1585,18 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       }));
       return PBFTV_OK;
     };
+    // an armed kernel that has left (budget, cancel, halt) is collected first
+    if (d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == d.arm_seq) {
+      HIP_TRY(set_dev());
+      HIP_TRY(qc_disarm(d));
+    }
     uint32_t cur = 0;  // the armed request number serving this call
-    const bool armable = n <= QcMail::kQcSlots;
-    if (armable && d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) != d.arm_seq) {
+    if (n <= QcMail::kQcSlots && d.arm_seq) {
       cur = d.arm_seq;
-      d.arm_seq = 0;
-      // the first signatures' slots: each line's data, then its tag (a line is
-      // read by the GPU as one snapshot, and x86 stores become visible in order)
+      // the kernel waits for cur + 1 next (0 is "none": cancel it at the wrap)
+      d.arm_seq = d.seq_counter = cur + 1;
+      // the slots: each line's data, then its tags (a line is read by the GPU
+      // as one snapshot, and x86 stores become visible in order)
       for (uint32_t i = 0; i < QcMail::kQcSlots; ++i) {
         uint32_t* l0 = reinterpret_cast<uint32_t*>(st8 + QcMail::slot_off(i));
         uint32_t* l1 = l0 + 16;
@@ -1386,12 +1616,12 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       __atomic_store_n(&m->bell, cur, __ATOMIC_RELEASE);  // inputs and n are in: ring
     } else {
       // a batch the armed kernel cannot take (n > its slots) leaves it armed
-      // for the next small one; an expired one is collected first
-      if (d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == d.arm_seq) HIP_TRY(qc_disarm(d));
+      // for the next small one
       int rc = launch_plain();
       if (rc != PBFTV_OK) return rc;
+      if (small) HIP_TRY(qc_arm(d));  // the next call's server (no-op while one is armed)
     }
-    if (small) HIP_TRY(qc_arm(d));  // the next call's kernel (no-op while one is armed)
+    const auto h_bell = std::chrono::steady_clock::now();
     // every wave writes its byte after its last read of the inputs, so once
     // all n bytes are in, the mailbox is free for the next call
     auto t0 = std::chrono::steady_clock::now();
@@ -1401,9 +1631,10 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         continue;
       }
       if (cur && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == cur) {
-        // the armed kernel gave up (budget or cancel) before it saw the bell:
-        // cancel its successor, wait for both to leave, then launch
-        HIP_TRY(qc_disarm(d));  // (waits for both armed kernels to leave)
+        // the armed kernel left (budget, cancel, halt) before it saw the bell:
+        // wait for the armed kernels to leave, then launch
+        HIP_TRY(set_dev());
+        HIP_TRY(qc_disarm(d));
         cur = 0;
         std::memset(const_cast<uint8_t*>(res), 0xFF, n);
         int rc = launch_plain();
@@ -1414,14 +1645,33 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         continue;
       }
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-        HIP_TRY(hipStreamSynchronize(d.stream));  // surfaces a kernel fault
+        // nothing that served (or could still serve) this call may outlive the
+        // return: the armed kernels and the launched one have left after these
+        // synchronisations (a kernel fault surfaces here), so no stale verdict
+        // can land in the next call's result bytes
+        HIP_TRY(set_dev());
+        HIP_TRY(qc_disarm(d));
+        HIP_TRY(hipStreamSynchronize(d.stream));
         for (uint64_t i = next; i < n; ++i)
           if (res[i] == 0xFF) return fail(PBFTV_EDEVICE, "wave verify kernel did not report every signature");
         break;
       }
     }
+    if (d.keeper_idle) {  // past its keep window: a call makes it keep the kernel armed again
+      d.keeper_idle = false;
+      d.keeper_cv.notify_one();
+    }
+    if (cur && d.arm_seq == 0) {  // the served number was 2^32 - 1: the kernel now waits for 0
+      __atomic_store_n(&m->stop, 0u, __ATOMIC_RELEASE);
+      HIP_TRY(set_dev());
+      HIP_TRY(qc_disarm(d));
+    }
     std::memset(out_bitmap, 0, (n + 7) / 8);
     for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((res[i] & 1u) << (i & 7));
+    const auto h_out = std::chrono::steady_clock::now();
+    d.qc_ns_handover = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(h_bell - h_in).count();
+    d.qc_ns_total = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(h_out - h_in).count();
+    d.qc_armed_served = cur != 0;
     return PBFTV_OK;
   }
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
@@ -1430,6 +1680,25 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     return verify_host_pipelined(d, hashes + 32 * s.lo, sig_rs + 64 * s.lo,
                                  key_idx + s.lo, s.hi - s.lo, out_bitmap + s.lo / 8);
   });
+}
+
+int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || !out) return fail(PBFTV_EINVAL, "bad context, device index or out pointer");
+  std::lock_guard<std::mutex> lk(d->mu);
+  std::memset(out, 0, 8 * sizeof(uint64_t));
+  out[0] = d->qc_ns_handover;
+  out[1] = d->qc_ns_total;
+  out[2] = d->qc_armed_served ? 1 : 0;
+  if (d->qc_armed_served && d->stage.p) {
+    const volatile uint64_t* st = reinterpret_cast<const volatile uint64_t*>(
+        d->stage.as<uint8_t>() + QcMail::stamps_off(qc_mail(*d)->cap));
+    for (int i = 0; i < 4; ++i) out[3 + i] = st[i];
+  }
+  int khz = 100000;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d->id);
+  out[7] = (uint64_t)khz;
+  return PBFTV_OK;
 }
 
 int pbftv_qc_verify(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs, const uint32_t* key_idx, uint64_t n,

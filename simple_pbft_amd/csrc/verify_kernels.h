@@ -1163,84 +1163,110 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
 }
 
 // ---- the armed latency kernel ------------------------------------------------
-// Launched AHEAD of the request it serves (pbftv_api.cpp arms one while the
-// previous request computes), so no launch is on the critical path.  One wave
-// per signature slot (QcMail::kQcSlots = 8: a certificate of n = 3f+1 <= 9
-// replicas).  Each wave polls, in ONE wave-wide load (lane l reads dword
-// l % 16 of line l / 16), the three 64-B lines of its slot and the mailbox
-// header: every slot line carries the request number in its first and last
-// dword, written by the host after the line's data (one line is read as one
-// snapshot of the host's cache line, and x86 stores become visible in order;
-// requiring both tags also covers a read that tore a line in two), so three
-// matching lines mean n, the key and the hash / r / s are already in
-// registers -- no second PCIe round trip.  Every wave reaches an exit: its
-// request (tags == want), a cancel (header stop == want) or the budget
-// (wall-clock ticks); a wave that leaves without serving writes
-// expired = want and the host serves the request with a launch instead.
-// Waits are s_sleep between polls; host words are read with system-scope
-// loads; nothing is written through the scalar cache.  The key tables'
-// pointers and validity flags of the first 128 keys are loaded while waiting.
+// A persistent server, launched AHEAD of the requests it serves (pbftv_api.cpp
+// keeps one armed per device), so neither a launch nor a re-arm is on a
+// certificate's critical path: after request `want` it waits for want + 1.
+// One wave per signature slot (QcMail::kQcSlots = 8: a certificate of
+// n = 3f+1 <= 9 replicas).  Each wave polls, in ONE wave-wide load (lane l
+// reads dword l % 16 of line l / 16), the three 64-B lines of its slot and the
+// mailbox header: every slot line carries the request number in its first and
+// last dword, written by the host after the line's data (one line is read as
+// one snapshot of the host's cache line, and x86 stores become visible in
+// order; requiring both tags also covers a read that tore a line in two), so
+// three matching lines mean n, the key and the hash / r / s are already in
+// registers -- no second PCIe round trip.  Waves with slots >= n go straight
+// back to waiting.  Every wave reaches an exit: a cancel (header stop == the
+// request number it waits for, or a change of the header's halt word) or the
+// budget (wall-clock ticks since launch); a wave that leaves writes
+// expired = that number, and the host serves a request that raced the exit
+// with a launch instead.  Waits are s_sleep between polls (spin: see
+// ArmArgs); host words are read with system-scope loads; nothing is written
+// through the scalar cache.  The key tables' pointers and validity flags of
+// the first 128 keys are loaded once, at launch (a key change cancels first).
 template <int WG, int WQ>
 __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ mail, uint32_t want, uint64_t budget,
                                                          const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                          const uint4* __restrict__ gtab,
-                                                         const uint4* const* __restrict__ qtabs) {
+                                                         const uint4* const* __restrict__ qtabs, uint32_t spin,
+                                                         uint32_t halt) {
   const uint32_t b = blockIdx.x, lane = threadIdx.x;
   const uint64_t t0 = wall_clock64();
+  if (b == 0 && lane == 0) reinterpret_cast<volatile uint32_t*>(mail)[6] = want;  // live: resident now
   // key data for keys < 128, two per lane (lane l: keys l and l + 64)
   const uint4* qt_lo = lane < nkeys ? qtabs[lane] : nullptr;
   const uint4* qt_hi = lane + 64 < nkeys ? qtabs[lane + 64] : nullptr;
   const uint32_t kv_lo = lane < nkeys ? key_valid[lane] : 0u, kv_hi = lane + 64 < nkeys ? key_valid[lane + 64] : 0u;
-  const uint8_t* base = reinterpret_cast<const uint8_t*>(mail);
+  uint8_t* const base = reinterpret_cast<uint8_t*>(mail);
   const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b));
   const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
-  uint32_t v = 0;
-  bool serve = false;
-  for (;;) {
-    v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (__builtin_amdgcn_readlane(v, 0) == want && __builtin_amdgcn_readlane(v, 15) == want &&
-        __builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
-        __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want) {
-      serve = true;
-      break;
+  for (;; ++want) {
+    uint32_t v = 0;
+    bool serve = false;
+    for (;;) {
+      v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (__builtin_amdgcn_readlane(v, 0) == want && __builtin_amdgcn_readlane(v, 15) == want &&
+          __builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
+          __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want) {
+        serve = true;
+        break;
+      }
+      if (__builtin_amdgcn_readlane(v, 48 + 2) == want || __builtin_amdgcn_readlane(v, 48 + 5) != halt ||
+          wall_clock64() - t0 > budget)
+        break;  // header stop / halt, or the budget
+      if (spin == 0) {
+        __builtin_amdgcn_s_sleep(2);
+      } else if (spin > 1) {
+        uint32_t x = lane;
+        for (uint32_t j = 0; j < spin; ++j) asm volatile("v_mad_u32_u24 %0, %0, %0, %0" : "+v"(x));
+      }
     }
-    if (__builtin_amdgcn_readlane(v, 48 + 2) == want || wall_clock64() - t0 > budget) break;  // header stop
-    __builtin_amdgcn_s_sleep(2);
+    if (!serve) {
+      if (lane == 0) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    const uint64_t seen_wall = wall_clock64(), seen_clk = clock64();
+    const uint32_t n = __builtin_amdgcn_readlane(v, 1);
+    if (b >= n) continue;
+    uint32_t e[8], r[8], s[8];
+    const uint32_t k = __builtin_amdgcn_readlane(v, 2);
+    PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // slot line j, dword 4 + t = LE dword t of the hash / r / s
+      e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 4 + t));
+      r[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 20 + t));
+      s[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 36 + t));
+    }
+    bool key_ok;
+    const uint4* qtab;
+    if (k < 128 && k < nkeys) {  // prefetched
+      const int kl = (int)(k & 63);
+      const uint64_t ql = (uint64_t)(uintptr_t)(k < 64 ? qt_lo : qt_hi);
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ql, kl),
+                     hi = __builtin_amdgcn_readlane((uint32_t)(ql >> 32), kl);
+      qtab = reinterpret_cast<const uint4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+      key_ok = __builtin_amdgcn_readlane(k < 64 ? kv_lo : kv_hi, kl) != 0;
+    } else {
+      key_ok = k < nkeys && key_valid[k] != 0;
+      qtab = qtabs[k < nkeys ? k : 0];
+    }
+    const bool ok = wave_verify_words<WG, WQ>(e, r, s, key_ok, gtab, qtab);
+    if (lane == 0) {
+      const uint32_t cap = __hip_atomic_load(&mail->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      volatile uint64_t* st = reinterpret_cast<volatile uint64_t*>(base + QcMail::stamps_off(cap)) + 4 * b;
+      st[0] = seen_wall;  // diagnostics (pbftv_qc_stamps), before the verdict
+      st[1] = seen_clk;
+      st[2] = wall_clock64();
+      st[3] = clock64();
+      // (coherent host memory is not cached on the GPU: the stores leave in
+      // order; a system-scope release here would write back the L2 first)
+      reinterpret_cast<volatile uint8_t*>(base)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
+    }
   }
-  if (!serve) {
-    if (lane == 0) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
-  const uint32_t n = __builtin_amdgcn_readlane(v, 1);
-  if (b >= n) return;
-  uint32_t e[8], r[8], s[8];
-  const uint32_t k = __builtin_amdgcn_readlane(v, 2);
-  PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // slot line j, dword 4 + t = LE dword t of the hash / r / s
-    e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 4 + t));
-    r[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 20 + t));
-    s[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 36 + t));
-  }
-  bool key_ok;
-  const uint4* qtab;
-  if (k < 128 && k < nkeys) {  // prefetched
-    const int kl = (int)(k & 63);
-    const uint64_t ql = (uint64_t)(uintptr_t)(k < 64 ? qt_lo : qt_hi);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ql, kl), hi = __builtin_amdgcn_readlane((uint32_t)(ql >> 32), kl);
-    qtab = reinterpret_cast<const uint4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
-    key_ok = __builtin_amdgcn_readlane(k < 64 ? kv_lo : kv_hi, kl) != 0;
-  } else {
-    key_ok = k < nkeys && key_valid[k] != 0;
-    qtab = qtabs[k < nkeys ? k : 0];
-  }
-  const bool ok = wave_verify_words<WG, WQ>(e, r, s, key_ok, gtab, qtab);
-  if (lane == 0) reinterpret_cast<volatile uint8_t*>(mail)[QcMail::res_off(mail->cap) + b] = ok ? 1 : 0;
 }
 
 template <int WG, int WQ>
 void launch_armed_w(const ArmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3(QcMail::kQcSlots), dim3(64), 0, st, a.mail, a.want, a.budget,
                      a.key_valid, a.nkeys, reinterpret_cast<const uint4*>(a.gtab),
-                     reinterpret_cast<const uint4* const*>(a.qtabs));
+                     reinterpret_cast<const uint4* const*>(a.qtabs), a.spin, a.halt);
 }
 
 template <int WG, int WQ>

@@ -72,6 +72,7 @@ def lib() -> ctypes.CDLL:
         "pbftv_kernel_time_ms": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_uint64)]),
         "pbftv_reset_kernel_times": (ctypes.c_int, [_vp]),
+        "pbftv_qc_stamps": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
         "pbftv_hash_hex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_char_p]),
         "pbftv_sha256_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
         "pbftv_digest_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
@@ -545,6 +546,19 @@ class Verifier:
 
     def reset_kernel_times(self):
         _check(self._L.pbftv_reset_kernel_times(self._h))
+
+    def qc_stamps(self, dev: int = 0) -> dict:
+        """pbftv_qc_stamps: where the last latency-path call's time went (host
+        hand-over / total in us; for an armed serve, the GPU's own serve time
+        and the mean shader clock over it)."""
+        o = np.zeros(8, np.uint64)
+        _check(self._L.pbftv_qc_stamps(self._h, dev, o.ctypes.data))
+        r = {"handover_us": float(o[0]) * 1e-3, "total_us": float(o[1]) * 1e-3, "armed": bool(o[2])}
+        if o[2] and o[5] > o[3]:
+            wall_s = float(o[5] - o[3]) / (float(o[7]) * 1e3)
+            r["gpu_serve_us"] = wall_s * 1e6
+            r["sclk_mhz"] = float(o[6] - o[4]) / wall_s * 1e-6
+        return r
 
     # ---- sha256 / digests
     def hash_hex(self, content: bytes) -> str:

@@ -164,3 +164,53 @@ def test_config1_every_message_signed(ver, oracle_lib):
     req_d = [hashlib.sha256(gojson.request(q[0], q[1], q[2], int(a))).digest()
              for q, a in zip(c["requests"], c["assigned_seqs"])]
     assert [bytes(x) for x in got["request_digests"]] == [req_d[j] for j in idx["request"]]
+
+
+def _openssl_sha256(data, off, ln):
+    """The checker: OpenSSL 3 EVP SHA-256 on host threads
+    (oracle/openssl_standin.c, built by __graft_entry__.build())."""
+    import ctypes
+    so = os.path.join(ROOT, "oracle", "libopenssl_standin.so")
+    L = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    L.standin_sha256_batch.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_int]
+    n = len(ln)
+    out = np.zeros((n, 32), np.uint8)
+    assert L.standin_sha256_batch(data.ctypes.data, off.ctypes.data, ln.ctypes.data, n, out.ctypes.data, 16) == 0
+    return out
+
+
+def test_config5_full_size_sha256(ver):
+    """configs[4] at its full size through the device API: 1,000,000 messages
+    of 256-4096 B (2.18 GB, so the last ~1.5 % start past 2^31 and their
+    offsets need all 64 bits) in ONE pbftv_sha256_batch_dev call, every digest
+    against OpenSSL (and a sample against hashlib), then 1 % of the expected
+    digests flipped and the match bitmap checked bit for bit."""
+    import hashlib
+    data, off, ln = synth.sha_config5(1_000_000)
+    n = len(ln)
+    assert int(off[-1]) + int(ln[-1]) > 2 ** 31 and (off >= 2 ** 31).sum() > 10_000
+    want = _openssl_sha256(data, off, ln)
+    rng = np.random.default_rng(5)
+    for i in list(rng.integers(0, n, 200)) + list(np.nonzero(off >= 2 ** 31)[0][[0, -1]]):
+        assert want[i].tobytes() == hashlib.sha256(data[off[i]:off[i] + ln[i]].tobytes()).digest()
+    exp = want.copy()
+    flip = rng.choice(n, n // 100, replace=False)
+    exp[flip, rng.integers(0, 32, len(flip))] ^= np.uint8(0x10)
+    dd = ver.to_device(0, data, pad=64)
+    do, dl, de = ver.to_device(0, off), ver.to_device(0, ln), ver.to_device(0, exp)
+    dord, dg, db = ver.alloc(0, 4 * n), ver.alloc(0, 32 * n), ver.alloc(0, (n + 31) // 32 * 4)
+    try:
+        ver.sha256_order_dev(0, dl.ptr, n, dord.ptr)
+        ver.sha256_batch_dev(0, dd.ptr, do.ptr, dl.ptr, dord.ptr, n, dg.ptr, de.ptr, db.ptr)
+        ver.sync(0)
+        got = dg.to_host().reshape(n, 32)
+        bad = np.nonzero((got != want).any(1))[0]
+        assert len(bad) == 0, (len(bad), bad[:10], off[bad[:10]])
+        bits = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
+        ok = np.ones(n, bool)
+        ok[flip] = False
+        assert (bits == ok).all()
+    finally:
+        for b in (dd, do, dl, de, dord, dg, db):
+            b.free()

@@ -496,16 +496,22 @@ def test_armed_path_golden_and_crafted(ecdsa_fixtures):
 
 
 
-@pytest.mark.parametrize("arm_ms", ["500", "1"])
-def test_armed_latency_path(oracle_lib, arm_ms, monkeypatch):
-    """Small host-buffer batches are served by the kernel armed at the end of
-    the previous call (doorbell in host memory).  Consecutive calls of every
-    size up to the mailbox capacity and past it, a key change while armed,
-    and -- with a 1 ms budget and pauses -- the armed kernel expiring so the
-    request falls back to a fresh launch; every bitmap against the oracle."""
+@pytest.mark.parametrize("mode", ["keeper", "expiring"])
+def test_armed_latency_path(oracle_lib, mode, monkeypatch):
+    """Small host-buffer batches are served by the persistent armed kernel
+    (doorbell in host memory).  Consecutive calls of every size up to the
+    mailbox capacity and past it, a key change while armed, and pauses longer
+    than the armed kernel's budget: with the keeper (mode "keeper", 20 ms
+    budget) the kernel is replaced before it runs out and every small call is
+    still served armed; without it (PBFTV_QC_KEEP_MS=0, 1 ms budget) the armed
+    kernel expires during each pause and the request must fall back to a
+    launch (pbftv_qc_stamps says which served it).  Every bitmap against the
+    oracle."""
     import time
     from simple_pbft_amd import Verifier
-    monkeypatch.setenv("PBFTV_QC_ARM_MS", arm_ms)
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", "20" if mode == "keeper" else "1")
+    if mode == "expiring":
+        monkeypatch.setenv("PBFTV_QC_KEEP_MS", "0")
     keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=5, per_key=60, seed=77)
     sigs[::7, 45] ^= 0x20
     n_all = len(kidx)
@@ -514,19 +520,69 @@ def test_armed_latency_path(oracle_lib, arm_ms, monkeypatch):
                                               keys.ctypes.data, len(keys), want.ctypes.data, 8)
     want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
     rng = np.random.default_rng(78)
+    served = []
     with Verifier(device_mask=1) as v:
         v.register_keys(keys)
-        for it, n in enumerate([1, 3, 3, 67, 128, 129, 300, 2, 64, 5, 127, 1, 3]):
+        for it, n in enumerate([1, 3, 3, 67, 128, 129, 300, 2, 64, 5, 127, 1, 3, 8, 4, 7]):
             o = rng.choice(n_all, n, replace=False)
             got = v.verify_batch(hashes[o], sigs[o], kidx[o])
             assert (got == want[o]).all(), (it, n)
-            if arm_ms == "1" and it % 3 == 1:
-                time.sleep(0.01)  # let the armed kernel expire
+            if n <= 8 and it > 0:
+                served.append((it, v.qc_stamps(0)["armed"]))
+            time.sleep(0.06)  # three budgets (keeper) / sixty (expiring)
+        if mode == "keeper":
+            assert all(a for _, a in served), served  # the keeper kept one armed through every pause
+        else:
+            assert not any(a for _, a in served), served  # every one expired: launched instead
         # a key change while a kernel is armed: it is cancelled first
         assert v.set_key(0, keys[0])
         o = rng.choice(n_all, 3, replace=False)
         assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all()
+        armed = 0
         for _ in range(200):  # back to back, the quorum count too
             o = rng.choice(n_all, 3, replace=False)
             bm, acc, ok = v.qc_verify(hashes[o], sigs[o], kidx[o], quorum=3)
             assert (bm == want[o]).all() and acc == int(want[o].sum()) and ok == bool(want[o].all())
+            armed += v.qc_stamps(0)["armed"]
+        assert armed >= (190 if mode == "keeper" else 0)
+
+
+def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypatch):
+    """An armed kernel with a 5-s budget stays resident between calls.  A
+    device free, a pinned-host free, and another context's key change on the
+    same GPU (hipDeviceSynchronize) must not wait for it: the library quiesces
+    the GPU (halts every armed kernel on it) first.  The halted context's next
+    call falls back to a launch and is still right."""
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", "5000")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=4, per_key=20, seed=81)
+    sigs[::5, 40] ^= 0x08
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    with Verifier(device_mask=1) as a, Verifier(device_mask=1) as b:
+        a.register_keys(keys)
+        b.register_keys(keys)
+        for v in (a, b):
+            for i in range(0, 12, 3):
+                assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
+        buf = a.alloc(0, 1 << 20)
+        t0 = time.perf_counter()
+        buf.free()
+        assert time.perf_counter() - t0 < 0.5
+        pin = a.pinned(np.zeros(1 << 16, np.uint8))
+        t0 = time.perf_counter()
+        pin.free()
+        assert time.perf_counter() - t0 < 0.5
+        for i in range(12, 24, 3):  # both contexts re-armed (or launched) and right
+            assert (a.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
+            assert (b.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
+        t0 = time.perf_counter()
+        assert b.set_key(1, keys[1])  # device synchronisation with a's kernel armed
+        assert time.perf_counter() - t0 < 2.0
+        for i in range(24, n_all - 3, 3):
+            for v in (a, b):
+                assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all(), i
