@@ -239,7 +239,9 @@ def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int, gap
     out = {"p50": float(np.percentile(us, 50)), "p90": float(np.percentile(us, 90)),
            "p99": float(np.percentile(us, 99)), "min": float(us.min()), "calls": iters, "gap_s": gap_s}
     out["in_library_us_p50"] = float(np.median(stamps[:, 1])) * 1e-3
-    armed = stamps[:, 2] == 1
+    out["in_library_handover_us_p50"] = float(np.median(stamps[:, 0])) * 1e-3
+    out["in_library_to_lock_us_p50"] = float(np.median(stamps[:, 2] >> np.uint64(32))) * 1e-3
+    armed = (stamps[:, 2] & np.uint64(1)) == 1
     out["armed_frac"] = float(armed.mean())
     if armed.any():
         a = stamps[armed].astype(np.float64)
@@ -251,6 +253,81 @@ def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int, gap
 
 def lib_handle(ver: Verifier):
     return ver._L
+
+
+def qc_under_load(ver: Verifier, dh, ds, dk, n: int, ok, seed: int, calls3: int = 300, calls67: int = 100):
+    """QC latency (2 ms between certificates) with the GPU idle and then with a
+    stream of 1M-signature batches running on another library stream of the
+    same context (a background thread enqueues two batches, waits, repeats):
+    what a certificate costs while the node also drains a large pool snapshot.
+    Certificates are signed by the registered config-4 committee (its keys:
+    synth.certs with the same seed)."""
+    import threading
+    _, H3, S3, K3 = synth.certs(100, 3, 2 * calls3 + 40, seed)
+    _, H67, S67, K67 = synth.certs(100, 67, 2 * calls67 + 20, seed)
+
+    def part(H, S, K, sigs, lo, cnt):
+        sl = slice(lo * sigs, (lo + cnt + 10) * sigs)
+        return qc_latency(ver, 100, sigs, cnt, 0, gap_s=0.002, warm=10, certs=(H[sl], S[sl], K[sl]))
+    out = {"idle_3sigs": part(H3, S3, K3, 3, 0, calls3), "idle_67sigs": part(H67, S67, K67, 67, 0, calls67)}
+    st = ver.stream_create(0)
+    db = ver.alloc(0, n // 8 + 1)
+    stop = threading.Event()
+    done = [0]
+
+    def stream():
+        while not stop.is_set():
+            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr, stream=st)
+            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr, stream=st)
+            ver.stream_wait(0, st)
+            done[0] += 2
+    th = threading.Thread(target=stream)
+    th.start()
+    try:
+        time.sleep(0.05)
+        t0 = time.perf_counter()
+        b0 = done[0]
+        out["loaded_3sigs"] = part(H3, S3, K3, 3, calls3 + 20, calls3)
+        out["loaded_67sigs"] = part(H67, S67, K67, 67, calls67 + 10, calls67)
+        out["stream_verifies_per_s_during"] = (done[0] - b0) * n / (time.perf_counter() - t0)
+    finally:
+        stop.set()
+        th.join()
+    out["stream_check"] = bool((np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool) == ok).all())
+    db.free()
+    ver.stream_destroy(0, st)
+    out["p50_ratio_3sigs"] = out["loaded_3sigs"]["p50"] / out["idle_3sigs"]["p50"]
+    out["p50_ratio_67sigs"] = out["loaded_67sigs"]["p50"] / out["idle_67sigs"]["p50"]
+    return out
+
+
+def cpu_qc_latency(threads_allot: int, tick_calls: int = 15):
+    """The CPU side of the QC-latency metric ("p50 QC verify
+    latency ... single-threaded per QC"): the OpenSSL stand-in verifying ONE
+    certificate at a time (oracle/openssl_standin.c standin_qc_latency: the
+    caller's thread plus persistent spinning workers, keys parsed once, as a
+    replica holds its peers' public keys), back to back and with the
+    reference's 1-s gap before each certificate.  p50 in us."""
+    so = os.path.join(ROOT, "oracle", "libopenssl_standin.so")
+    if not os.path.exists(so):
+        return None
+    L = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    L.standin_qc_latency.restype = ctypes.c_int64
+    L.standin_qc_latency.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint32, ctypes.c_int,
+                                     ctypes.c_double, vp, vp]
+    out = {"kind": "openssl_standin", "threads_allotment": threads_allot}
+    for nk, sg, thr, cnt, gap in ((4, 3, 1, 400, 0.0), (4, 3, 3, 400, 0.0), (100, 67, threads_allot, 200, 0.0),
+                                  (100, 67, 1, 30, 0.0), (4, 3, 1, tick_calls, 1.0), (4, 3, 3, tick_calls, 1.0)):
+        pub, H, S, K = synth.certs(nk, sg, cnt, 21 + nk)
+        us = np.zeros(cnt)
+        bm = np.zeros((cnt * sg + 7) // 8, np.uint8)
+        acc = L.standin_qc_latency(H.ctypes.data, S.ctypes.data, K.ctypes.data, cnt, sg, pub.ctypes.data, len(pub),
+                                   thr, gap * 1e6, us.ctypes.data, bm.ctypes.data)
+        assert acc == cnt * sg, (acc, cnt * sg)
+        key = f"n{nk}_{sg}sigs_{thr}thr" + ("_tick" if gap else "")
+        out[key] = {"p50": float(np.percentile(us, 50)), "p99": float(np.percentile(us, 99)), "calls": cnt}
+    return out
 
 
 def cpu_model() -> str:
@@ -847,19 +924,46 @@ def main():
         out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
         out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "what": "pbftv_register_keys: G table + the key tables built on the device (incl. allocation)"}
         if not args.no_extras and ws == 1:
+            # host-buffer path with no armed latency kernel on the GPU (none armed yet)
             out["host_path"] = host_path(ver, H, S, K, ok)
             out["host_path_verifies_per_s"] = out["host_path"]["pageable"]["verifies_per_s"]
-            p50_4, p99_4 = qc_latency(ver, 4, 3, 10000, 11)
-            p50_100, p99_100 = qc_latency(ver, 100, 67, 2000, 12)
-            out["qc_latency_us"] = {"p50_n4_3sigs": p50_4, "p99_n4_3sigs": p99_4, "p50_n100_67sigs": p50_100,
-                                    "p99_n100_67sigs": p99_100, "calls": {"n4": 10000, "n100": 2000},
-                                    "definition": "host submit -> accept bitmap + quorum on host, pbftv_qc_verify, "
-                                                  "one certificate per call (SURVEY.md §8(d))"}
+            # certificates while a 1M stream runs on another stream of this context
+            load = qc_under_load(ver, dh, ds, dk, n, ok, seed=0x50424654)
+            # ... and the host path again with the armed kernel kept waiting
+            # (the keeper holds one for PBFTV_QC_KEEP_MS after the last call)
+            hp_armed = host_path(ver, H, S, K, ok)
+            out["host_path_with_armed_kernel"] = {
+                **hp_armed, "ratio_pageable": hp_armed["pageable"]["verifies_per_s"] /
+                out["host_path"]["pageable"]["verifies_per_s"],
+                "ratio_pinned": hp_armed["pinned"]["verifies_per_s"] / out["host_path"]["pinned"]["verifies_per_s"]}
+            q4 = qc_latency(ver, 4, 3, 10000, 11)
+            q4_tick = qc_latency(ver, 4, 3, 30, 13, gap_s=1.0, warm=3)
+            q4_100 = qc_latency(ver, 4, 3, 30, 14, gap_s=0.1, warm=3)
+            q100 = qc_latency(ver, 100, 67, 2000, 12)
+            q100_tick = qc_latency(ver, 100, 67, 20, 15, gap_s=1.0, warm=3)
+            out["qc_latency_us"] = {
+                "p50_n4_3sigs": q4["p50"], "p99_n4_3sigs": q4["p99"],
+                "p50_n100_67sigs": q100["p50"], "p99_n100_67sigs": q100["p99"],
+                "p50_n4_3sigs_tick": q4_tick["p50"], "p50_n4_3sigs_gap100ms": q4_100["p50"],
+                "p50_n100_67sigs_tick": q100_tick["p50"],
+                "tick_over_back_to_back_n4": q4_tick["p50"] / q4["p50"],
+                "tick_over_back_to_back_n100": q100_tick["p50"] / q100["p50"],
+                "p50_n4_3sigs_under_1M_stream": load["loaded_3sigs"]["p50"],
+                "p50_n100_67sigs_under_1M_stream": load["loaded_67sigs"]["p50"],
+                "calls": {"n4": q4["calls"], "n100": q100["calls"], "n4_tick": q4_tick["calls"],
+                          "n4_gap100ms": q4_100["calls"], "n100_tick": q100_tick["calls"]},
+                "definition": "host submit -> accept bitmap + quorum on host, pbftv_qc_verify, one FRESH "
+                              "certificate per call (SURVEY.md §8(d)), called from C (tools/qc_driver.c) as a cgo "
+                              "caller would; _tick = a 1-s idle gap before every call (the reference's alarm, "
+                              "pbft/network/node.go:44)",
+                "detail": {"n4": q4, "n4_tick": q4_tick, "n4_gap100ms": q4_100, "n100": q100, "n100_tick": q100_tick},
+                "under_load": load}
             # the CPU baseline on every host CPU this process may use (affinity
             # mask capped by the cgroup quota, with the evidence), plus the
             # 16-thread figure of the box's nominal per-GPU share as a labelled extra
             allot = cpu_allotment()
             thr = allot["threads"]
+            out["cpu_qc_latency_us"] = cpu_qc_latency(thr)
             sample = cpu_standin_sample(thr, n)
             cb = openssl_standin(pub, H, S, K, sample=sample, threads=thr)
             if cb is not None:

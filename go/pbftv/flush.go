@@ -67,10 +67,10 @@ func (x *Ctx) FlushVotes(votes []VoteMsg, sigs [][64]byte, keyIdx []uint32, stat
 	sv, sl, sd := stateColumns(states)
 	res := VoteResult{Digests: make([][32]byte, n)}
 	sbm, mbm := make([]byte, (n+7)/8+1), make([]byte, (n+7)/8+1)
-	rc := C.pbftv_flush_votes(x.c, C.uint64_t(n), i64(views), i64(seqs), u8(d.blob), u64(d.off), u32(d.ln),
+	err := call(func() C.int { return C.pbftv_flush_votes(x.c, C.uint64_t(n), i64(views), i64(seqs), u8(d.blob), u64(d.off), u32(d.ln),
 		u8(id.blob), u64(id.off), u32(id.ln), i64(types), sigPtr(sigs), u32(keyIdx), C.uint32_t(len(states)),
-		i64(sv), i64(sl), digestPtr(sd), u32(stateIdx), digestPtr(res.Digests), u8(sbm), u8(mbm))
-	if err := check(rc); err != nil {
+		i64(sv), i64(sl), digestPtr(sd), u32(stateIdx), digestPtr(res.Digests), u8(sbm), u8(mbm)) })
+	if err != nil {
 		return VoteResult{}, err
 	}
 	res.SigOK, res.MsgOK = bits(sbm, n), bits(mbm, n)
@@ -109,10 +109,10 @@ func (x *Ctx) FlushRequests(reqs []RequestMsg, sigs [][64]byte, keyIdx []uint32,
 		cons = digestPtr(res.ConsensusDigests)
 	}
 	sbm := make([]byte, (n+7)/8+1)
-	rc := C.pbftv_flush_requests(x.c, C.uint64_t(n), i64(ts), u8(cid.blob), u64(cid.off), u32(cid.ln), u8(op.blob),
+	err := call(func() C.int { return C.pbftv_flush_requests(x.c, C.uint64_t(n), i64(ts), u8(cid.blob), u64(cid.off), u32(cid.ln), u8(op.blob),
 		u64(op.off), u32(op.ln), i64(seqs), sigPtr(sigs), u32(keyIdx), i64(assigned), digestPtr(res.Digests),
-		u8(sbm), cons)
-	if err := check(rc); err != nil {
+		u8(sbm), cons) })
+	if err != nil {
 		return RequestResult{}, err
 	}
 	res.SigOK = bits(sbm, n)
@@ -137,10 +137,10 @@ func (x *Ctx) FlushReplies(reps []ReplyMsg, sigs [][64]byte, keyIdx []uint32) ([
 	cid, id, rs := packStrings(cids), packStrings(ids), packStrings(results)
 	dg := make([][32]byte, n)
 	sbm := make([]byte, (n+7)/8+1)
-	rc := C.pbftv_flush_replies(x.c, C.uint64_t(n), i64(views), i64(ts), u8(cid.blob), u64(cid.off), u32(cid.ln),
+	err := call(func() C.int { return C.pbftv_flush_replies(x.c, C.uint64_t(n), i64(views), i64(ts), u8(cid.blob), u64(cid.off), u32(cid.ln),
 		u8(id.blob), u64(id.off), u32(id.ln), u8(rs.blob), u64(rs.off), u32(rs.ln), sigPtr(sigs), u32(keyIdx),
-		digestPtr(dg), u8(sbm))
-	if err := check(rc); err != nil {
+		digestPtr(dg), u8(sbm)) })
+	if err != nil {
 		return nil, nil, err
 	}
 	return dg, bits(sbm, n), nil
@@ -182,11 +182,11 @@ func (x *Ctx) FlushPrePrepares(pps []PrePrepareMsg, sigs [][64]byte, keyIdx []ui
 	sv, sl, _ := stateColumns(states)
 	res := PrePrepareResult{Digests: make([][32]byte, n), ReqDigests: make([][32]byte, n)}
 	sbm, mbm := make([]byte, (n+7)/8+1), make([]byte, (n+7)/8+1)
-	rc := C.pbftv_flush_preprepares(x.c, C.uint64_t(n), i64(views), i64(seqs), u8(d.blob), u64(d.off), u32(d.ln),
+	err := call(func() C.int { return C.pbftv_flush_preprepares(x.c, C.uint64_t(n), i64(views), i64(seqs), u8(d.blob), u64(d.off), u32(d.ln),
 		u8(has), i64(rts), u8(cid.blob), u64(cid.off), u32(cid.ln), u8(op.blob), u64(op.off), u32(op.ln), i64(rseqs),
 		sigPtr(sigs), u32(keyIdx), C.uint32_t(len(states)), i64(sv), i64(sl), u32(stateIdx), digestPtr(res.Digests),
-		digestPtr(res.ReqDigests), u8(sbm), u8(mbm))
-	if err := check(rc); err != nil {
+		digestPtr(res.ReqDigests), u8(sbm), u8(mbm)) })
+	if err != nil {
 		return PrePrepareResult{}, err
 	}
 	res.SigOK, res.MsgOK = bits(sbm, n), bits(mbm, n)

@@ -26,6 +26,7 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"runtime"
 	"sync"
 	"unsafe"
 )
@@ -46,6 +47,15 @@ type Error struct {
 }
 
 func (e *Error) Error() string { return fmt.Sprintf("pbftv error %d: %s", e.Code, e.Msg) }
+
+// call runs one library call and reads its error message on the same OS
+// thread: pbftv_last_error is thread-local, and a goroutine can move to
+// another thread between two cgo calls.
+func call(f func() C.int) error {
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+	return check(f())
+}
 
 func check(rc C.int) error {
 	if rc == 0 {
@@ -73,7 +83,7 @@ type Ctx struct {
 // Open opens the GPUs in deviceMask (0 = every visible gfx950 GPU).
 func Open(deviceMask uint32) (*Ctx, error) {
 	var c *C.pbftv_ctx
-	if err := check(C.pbftv_open(&c, C.uint32_t(deviceMask))); err != nil {
+	if err := call(func() C.int { return C.pbftv_open(&c, C.uint32_t(deviceMask)) }); err != nil {
 		return nil, err
 	}
 	return &Ctx{c: c}, nil
@@ -97,6 +107,16 @@ var (
 )
 
 // Default is the process-wide context on every visible GPU, opened on first use.
+// MustInit opens the default context or panics with the library's reason
+// (ENODEV: no usable gfx950 GPU).  Call it once at replica start-up.
+func MustInit() *Ctx {
+	x, err := Default()
+	if err != nil {
+		panic(fmt.Sprintf("pbftv: the GPU verify path is unavailable (%v); this build has no CPU fallback", err))
+	}
+	return x
+}
+
 func Default() (*Ctx, error) {
 	defaultOnce.Do(func() { defaultCtx, defaultErr = Open(0) })
 	return defaultCtx, defaultErr
@@ -142,7 +162,10 @@ func bits(bm []byte, n int) []bool {
 
 // Hash keeps utils.Hash's signature (utils/utils.go:13-17): lowercase hex
 // SHA-256 of content, on the default context.  utils.Hash cannot fail, so a
-// library error panics.
+// library error panics -- including PBFTV_ENODEV on a host without a gfx950
+// GPU: there is deliberately no CPU fallback behind this path.  A replica
+// built with the drop-in calls MustInit at start-up, so a GPU-less host fails
+// there, before it joins consensus, not in its first digest().
 func Hash(content []byte) string {
 	x, err := Default()
 	if err != nil {
@@ -158,7 +181,7 @@ func Hash(content []byte) string {
 // Hash is utils.Hash on this context.
 func (x *Ctx) Hash(content []byte) (string, error) {
 	var out [65]C.char
-	if err := check(C.pbftv_hash_hex(x.c, u8(content), C.uint64_t(len(content)), &out[0])); err != nil {
+	if err := call(func() C.int { return C.pbftv_hash_hex(x.c, u8(content), C.uint64_t(len(content)), &out[0]) }); err != nil {
 		return "", err
 	}
 	return C.GoString(&out[0]), nil
@@ -200,9 +223,9 @@ func (x *Ctx) HashBatch(msgs [][]byte) ([][32]byte, error) {
 	}
 	c := packBytes(msgs)
 	out := make([][32]byte, n)
-	rc := C.pbftv_sha256_batch(x.c, u8(c.blob), u64(c.off), u32(c.ln), C.uint64_t(n),
-		(*C.uint8_t)(unsafe.Pointer(&out[0])))
-	return out, check(rc)
+	err := call(func() C.int { return C.pbftv_sha256_batch(x.c, u8(c.blob), u64(c.off), u32(c.ln), C.uint64_t(n),
+		(*C.uint8_t)(unsafe.Pointer(&out[0]))) })
+	return out, err
 }
 
 // ---------------------------------------------------------------- keys
@@ -219,7 +242,7 @@ func keyPtr(pubXY [][64]byte) *C.uint8_t {
 // order (pbft/network/node.go:60-65); valid[j] = key j is a P-256 point.
 func (x *Ctx) RegisterKeys(pubXY [][64]byte) ([]bool, error) {
 	valid := make([]byte, len(pubXY)+1)
-	if err := check(C.pbftv_register_keys(x.c, keyPtr(pubXY), C.uint32_t(len(pubXY)), u8(valid))); err != nil {
+	if err := call(func() C.int { return C.pbftv_register_keys(x.c, keyPtr(pubXY), C.uint32_t(len(pubXY)), u8(valid)) }); err != nil {
 		return nil, err
 	}
 	out := make([]bool, len(pubXY))
@@ -232,7 +255,7 @@ func (x *Ctx) RegisterKeys(pubXY [][64]byte) ([]bool, error) {
 // AddKeys appends keys after the registered ones (membership change).
 func (x *Ctx) AddKeys(pubXY [][64]byte) ([]bool, error) {
 	valid := make([]byte, len(pubXY)+1)
-	if err := check(C.pbftv_add_keys(x.c, keyPtr(pubXY), C.uint32_t(len(pubXY)), u8(valid))); err != nil {
+	if err := call(func() C.int { return C.pbftv_add_keys(x.c, keyPtr(pubXY), C.uint32_t(len(pubXY)), u8(valid)) }); err != nil {
 		return nil, err
 	}
 	out := make([]bool, len(pubXY))
@@ -245,7 +268,7 @@ func (x *Ctx) AddKeys(pubXY [][64]byte) ([]bool, error) {
 // SetKey replaces key index in place.
 func (x *Ctx) SetKey(index uint32, pubXY [64]byte) (bool, error) {
 	var valid C.uint8_t
-	err := check(C.pbftv_set_key(x.c, C.uint32_t(index), (*C.uint8_t)(unsafe.Pointer(&pubXY[0])), &valid))
+	err := call(func() C.int { return C.pbftv_set_key(x.c, C.uint32_t(index), (*C.uint8_t)(unsafe.Pointer(&pubXY[0])), &valid) })
 	return valid == 1, err
 }
 
@@ -262,9 +285,9 @@ func (x *Ctx) VerifySigs(hashes [][32]byte, sigs [][64]byte, keyIdx []uint32) ([
 		return nil, nil
 	}
 	bm := make([]byte, (n+7)/8)
-	rc := C.pbftv_ecdsa_p256_verify_batch(x.c, (*C.uint8_t)(unsafe.Pointer(&hashes[0])),
-		(*C.uint8_t)(unsafe.Pointer(&sigs[0])), u32(keyIdx), C.uint64_t(n), u8(bm))
-	if err := check(rc); err != nil {
+	err := call(func() C.int { return C.pbftv_ecdsa_p256_verify_batch(x.c, (*C.uint8_t)(unsafe.Pointer(&hashes[0])),
+		(*C.uint8_t)(unsafe.Pointer(&sigs[0])), u32(keyIdx), C.uint64_t(n), u8(bm)) })
+	if err != nil {
 		return nil, err
 	}
 	return bits(bm, n), nil
@@ -285,9 +308,9 @@ func (x *Ctx) QCVerify(hashes [][32]byte, sigs [][64]byte, keyIdx []uint32, quor
 	bm := make([]byte, (n+7)/8)
 	var acc C.uint64_t
 	var q C.int
-	rc := C.pbftv_qc_verify(x.c, (*C.uint8_t)(unsafe.Pointer(&hashes[0])), (*C.uint8_t)(unsafe.Pointer(&sigs[0])),
-		u32(keyIdx), C.uint64_t(n), C.uint32_t(quorum), u8(bm), &acc, &q)
-	if err := check(rc); err != nil {
+	err := call(func() C.int { return C.pbftv_qc_verify(x.c, (*C.uint8_t)(unsafe.Pointer(&hashes[0])), (*C.uint8_t)(unsafe.Pointer(&sigs[0])),
+		u32(keyIdx), C.uint64_t(n), C.uint32_t(quorum), u8(bm), &acc, &q) })
+	if err != nil {
 		return nil, 0, false, err
 	}
 	return bits(bm, n), int(acc), q != 0, nil
@@ -379,10 +402,10 @@ func VerifyMsgBatch(st State, viewIDs, seqIDs []int64, digestGot []string) ([]bo
 	}
 	c := packStrings(digestGot)
 	bm := make([]byte, (n+7)/8+1)
-	rc := C.pbftv_verify_msg_batch(C.int64_t(st.ViewID), C.int64_t(st.LastSequenceID),
+	err := call(func() C.int { return C.pbftv_verify_msg_batch(C.int64_t(st.ViewID), C.int64_t(st.LastSequenceID),
 		(*C.uint8_t)(unsafe.Pointer(&st.ReqDigest[0])), C.uint64_t(n), i64(viewIDs), i64(seqIDs),
-		(*C.char)(unsafe.Pointer(&c.blob[0])), u64(c.off), u32(c.ln), u8(bm))
-	if err := check(rc); err != nil {
+		(*C.char)(unsafe.Pointer(&c.blob[0])), u64(c.off), u32(c.ln), u8(bm)) })
+	if err != nil {
 		return nil, err
 	}
 	return bits(bm, n), nil

@@ -95,6 +95,13 @@ int pbftv_stream_create(pbftv_ctx* ctx, int dev, void** out_stream);
 int pbftv_stream_destroy(pbftv_ctx* ctx, int dev, void* stream);
 int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
 
+/* Batches of up to n signatures take the latency path (one wave per
+ * signature; the armed kernel for <= 8); larger ones the lane path (scalar +
+ * comb kernels).  Default 2048, or PBFTV_WAVE_MAX at pbftv_open; 0 disables
+ * the latency path.  Read once per call from the context, never from the
+ * environment on the call path. */
+int pbftv_set_latency_path_max(pbftv_ctx* ctx, uint64_t n);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every
  * kernel launch while enabled.  kernel: 0 = ecdsa scalars, 1 = ecdsa comb,
  * 2 = sha256, 3 = ecdsa wave-per-signature (small batches), 4 = Go-JSON message
@@ -110,8 +117,9 @@ int pbftv_kernel_time_ms(pbftv_ctx* ctx, int dev, int kernel, double* out_ms, ui
 int pbftv_reset_kernel_times(pbftv_ctx* ctx);
 /* Diagnostics of the last latency-path call (n <= 2048) on device dev:
  * out[0] = host ns from entry to the request being handed over (bell rung or
- * kernel launched), out[1] = host ns from entry to return, out[2] = 1 if an
- * armed kernel served it, 0 if a launch did, out[3..6] = the armed kernel's
+ * kernel launched), out[1] = host ns from entry to return, out[2] bit 0 = 1
+ * if an armed kernel served it, 0 if a launch did, out[2] >> 32 = host ns from
+ * entry to holding the device lock, out[3..6] = the armed kernel's
  * slot-0 wave: GPU wall clock and shader clock when it saw the request, and
  * when it wrote its verdict (0 after a launch), out[7] = the wall-clock rate
  * in kHz. */

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -226,7 +227,7 @@ struct Device {
   bool keeper_stop = false, keeper_idle = false;
   uint64_t rotations = 0;
   // diagnostics of the last latency-path call (pbftv_qc_stamps)
-  uint64_t qc_ns_handover = 0, qc_ns_total = 0;
+  uint64_t qc_ns_entry = 0, qc_ns_handover = 0, qc_ns_total = 0;
   bool qc_armed_served = false;
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
@@ -256,6 +257,7 @@ struct Device {
   std::map<hipStream_t, std::unique_ptr<VerifyScratch>> stream_scratch;
   // kernel timing (events recorded around launches while ctx timing is on)
   const bool* timing = nullptr;
+  const std::atomic<uint64_t>* wave_max = nullptr;  // the context's latency-path threshold
   static constexpr int kKernels = 5;  // PBFTV_K_*
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[kKernels];
   double acc_ms[kKernels] = {0, 0, 0, 0, 0};
@@ -540,6 +542,10 @@ std::map<std::pair<int, int>, GSlot> g_tables;
 struct pbftv_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   bool timing = false;
+  // batches up to this size take the latency path (PBFTV_WAVE_MAX at open,
+  // pbftv_set_latency_path_max): read once, not per call (a cold getenv cost
+  // a certificate ~3 us after an idle second)
+  std::atomic<uint64_t> wave_max{2048};
 };
 
 namespace {
@@ -779,12 +785,14 @@ int pbftv_open(pbftv_ctx** out, uint32_t device_mask) {
       auto dev = std::make_unique<Device>();
       dev->id = d;
       dev->timing = &ctx->timing;
+      dev->wave_max = &ctx->wave_max;
       HIP_TRY(hipSetDevice(d));
       HIP_TRY(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
       ctx->devs.push_back(std::move(dev));
     }
   }
   if (ctx->devs.empty()) return fail(PBFTV_ENODEV, "no gfx950 device in device_mask");
+  ctx->wave_max = pbftv::wave_path_max();
   *out = ctx.release();
   return PBFTV_OK;
 }
@@ -978,6 +986,12 @@ int pbftv_stream_sync(pbftv_ctx* ctx, int dev) {
   if (!d) return fail(PBFTV_EINVAL, "bad context or device index");
   HIP_TRY(hipSetDevice(d->id));
   HIP_TRY(hipStreamSynchronize(d->stream));
+  return PBFTV_OK;
+}
+
+int pbftv_set_latency_path_max(pbftv_ctx* ctx, uint64_t n) {
+  if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
+  ctx->wave_max.store(n, std::memory_order_relaxed);
   return PBFTV_OK;
 }
 
@@ -1380,7 +1394,7 @@ int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uin
 static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d_sigs, const uint32_t* d_key_idx,
                             uint64_t n, uint8_t* d_bitmap, hipStream_t st, VerifyScratch* own = nullptr) {
   if (!d.have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
-  if (n <= pbftv::wave_path_max()) {
+  if (n <= d.wave_max->load(std::memory_order_relaxed)) {
     HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, st, [&] {
       return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(),
                                       d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), d_bitmap, nullptr, st);
@@ -1532,11 +1546,12 @@ int pbftv_ecdsa_p256_verify_batch_dev(pbftv_ctx* ctx, int dev, const uint8_t* d_
 
 int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs,
                                   const uint32_t* key_idx, uint64_t n, uint8_t* out_bitmap) {
+  const auto h_entry = std::chrono::steady_clock::now();
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
   if (n && (!hashes || !sig_rs || !key_idx || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
   for (auto& dp : ctx->devs)
     if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
-  if (n && n <= pbftv::wave_path_max()) {
+  if (n && n <= ctx->wave_max.load(std::memory_order_relaxed)) {
     // latency path on the first device: inputs packed into pinned coherent
     // host memory (the QcMail mailbox) that the kernel reads directly, one byte
     // per signature written back the same way and polled for (sentinel 0xFF):
@@ -1606,12 +1621,14 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
           std::memcpy(l1 + 4, sig_rs + 64 * i, 32);
           std::memcpy(l2 + 4, sig_rs + 64 * i + 32, 32);
           l0[2] = key_idx[i];
+          for (uint32_t* l : {l1, l2}) {
+            __atomic_store_n(l + 15, cur, __ATOMIC_RELEASE);
+            __atomic_store_n(l, cur, __ATOMIC_RELEASE);
+          }
         }
-        l0[1] = (uint32_t)n;
-        for (uint32_t* l : {l1, l2, l0}) {
-          __atomic_store_n(l + 15, cur, __ATOMIC_RELEASE);
-          __atomic_store_n(l, cur, __ATOMIC_RELEASE);
-        }
+        l0[1] = (uint32_t)n;  // a slot past n: line 0 only (its wave reads n and waits for the next)
+        __atomic_store_n(l0 + 15, cur, __ATOMIC_RELEASE);
+        __atomic_store_n(l0, cur, __ATOMIC_RELEASE);
       }
       __atomic_store_n(&m->bell, cur, __ATOMIC_RELEASE);  // inputs and n are in: ring
     } else {
@@ -1669,8 +1686,12 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     std::memset(out_bitmap, 0, (n + 7) / 8);
     for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((res[i] & 1u) << (i & 7));
     const auto h_out = std::chrono::steady_clock::now();
-    d.qc_ns_handover = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(h_bell - h_in).count();
-    d.qc_ns_total = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(h_out - h_in).count();
+    auto ns = [](std::chrono::steady_clock::duration x) {
+      return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(x).count();
+    };
+    d.qc_ns_entry = ns(h_in - h_entry);
+    d.qc_ns_handover = ns(h_bell - h_entry);
+    d.qc_ns_total = ns(h_out - h_entry);
     d.qc_armed_served = cur != 0;
     return PBFTV_OK;
   }
@@ -1689,7 +1710,7 @@ int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]) {
   std::memset(out, 0, 8 * sizeof(uint64_t));
   out[0] = d->qc_ns_handover;
   out[1] = d->qc_ns_total;
-  out[2] = d->qc_armed_served ? 1 : 0;
+  out[2] = (d->qc_armed_served ? 1 : 0) | (std::min<uint64_t>(d->qc_ns_entry, 0xFFFFFFFFull) << 32);
   if (d->qc_armed_served && d->stage.p) {
     const volatile uint64_t* st = reinterpret_cast<const volatile uint64_t*>(
         d->stage.as<uint8_t>() + QcMail::stamps_off(qc_mail(*d)->cap));

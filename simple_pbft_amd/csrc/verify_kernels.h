@@ -1174,8 +1174,8 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
 // one snapshot of the host's cache line, and x86 stores become visible in
 // order; requiring both tags also covers a read that tore a line in two), so
 // three matching lines mean n, the key and the hash / r / s are already in
-// registers -- no second PCIe round trip.  Waves with slots >= n go straight
-// back to waiting.  Every wave reaches an exit: a cancel (header stop == the
+// registers -- no second PCIe round trip.  Waves with slots >= n need only
+// line 0 (n) and go straight back to waiting.  Every wave reaches an exit: a cancel (header stop == the
 // request number it waits for, or a change of the header's halt word) or the
 // budget (wall-clock ticks since launch); a wave that leaves writes
 // expired = that number, and the host serves a request that raced the exit
@@ -1204,9 +1204,12 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
     bool serve = false;
     for (;;) {
       v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // line 0 carries n; a slot past n needs only that line (the host writes
+      // no inputs there), a slot below n all three
       if (__builtin_amdgcn_readlane(v, 0) == want && __builtin_amdgcn_readlane(v, 15) == want &&
-          __builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
-          __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want) {
+          (b >= __builtin_amdgcn_readlane(v, 1) ||
+           (__builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
+            __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want))) {
         serve = true;
         break;
       }
@@ -1227,6 +1230,9 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
     const uint64_t seen_wall = wall_clock64(), seen_clk = clock64();
     const uint32_t n = __builtin_amdgcn_readlane(v, 1);
     if (b >= n) continue;
+    // a certificate's waves go ahead of whatever else shares their SIMDs (the
+    // waves of a large batch: issue priority only, nothing is preempted)
+    __builtin_amdgcn_s_setprio(3);
     uint32_t e[8], r[8], s[8];
     const uint32_t k = __builtin_amdgcn_readlane(v, 2);
     PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // slot line j, dword 4 + t = LE dword t of the hash / r / s
@@ -1259,6 +1265,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
       // order; a system-scope release here would write back the L2 first)
       reinterpret_cast<volatile uint8_t*>(base)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
     }
+    __builtin_amdgcn_s_setprio(0);
   }
 }
 

@@ -73,6 +73,7 @@ def lib() -> ctypes.CDLL:
                                                 ctypes.POINTER(ctypes.c_uint64)]),
         "pbftv_reset_kernel_times": (ctypes.c_int, [_vp]),
         "pbftv_qc_stamps": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
+        "pbftv_set_latency_path_max": (ctypes.c_int, [_vp, ctypes.c_uint64]),
         "pbftv_hash_hex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_char_p]),
         "pbftv_sha256_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
         "pbftv_digest_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
@@ -465,6 +466,20 @@ class Verifier:
         h = ctypes.c_void_p()
         _check(self._L.pbftv_open(ctypes.byref(h), device_mask))
         self._h = h
+        self._wave_env = os.environ.get("PBFTV_WAVE_MAX")  # what pbftv_open read
+
+    def set_latency_path_max(self, n: int):
+        """pbftv_set_latency_path_max: batches up to n take the latency path."""
+        _check(self._L.pbftv_set_latency_path_max(self._h, n))
+
+    def _sync_env(self):
+        # the library reads PBFTV_WAVE_MAX once, at pbftv_open (no getenv on its
+        # call path); tests flip the variable under one context, so the binding
+        # forwards a change before the calls that depend on it
+        e = os.environ.get("PBFTV_WAVE_MAX")
+        if e != self._wave_env:
+            self._wave_env = e
+            self.set_latency_path_max(int(e) if e is not None else 2048)
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -553,8 +568,10 @@ class Verifier:
         and the mean shader clock over it)."""
         o = np.zeros(8, np.uint64)
         _check(self._L.pbftv_qc_stamps(self._h, dev, o.ctypes.data))
-        r = {"handover_us": float(o[0]) * 1e-3, "total_us": float(o[1]) * 1e-3, "armed": bool(o[2])}
-        if o[2] and o[5] > o[3]:
+        armed = bool(int(o[2]) & 1)
+        r = {"handover_us": float(o[0]) * 1e-3, "total_us": float(o[1]) * 1e-3, "armed": armed,
+             "entry_us": float(int(o[2]) >> 32) * 1e-3}
+        if armed and o[5] > o[3]:
             wall_s = float(o[5] - o[3]) / (float(o[7]) * 1e3)
             r["gpu_serve_us"] = wall_s * 1e6
             r["sclk_mhz"] = float(o[6] - o[4]) / wall_s * 1e-6
@@ -643,6 +660,7 @@ class Verifier:
                     digests: bool = True):
         """pbftv_flush_votes: (digests | None, sig_ok | None, msg_ok | None).
         states: (view_ids int64[k], last_seqs int64[k], req_digests uint8[k, 32])."""
+        self._sync_env()
         n = cols.n
         nb = (n + 7) // 8 + 1
         out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
@@ -673,6 +691,7 @@ class Verifier:
     def flush_requests(self, cols: "RequestColumns", sigs=None, key_idx=None, assigned_seqs=None,
                        digests: bool = True):
         """pbftv_flush_requests: (digests | None, sig_ok | None, consensus digests | None)."""
+        self._sync_env()
         n = cols.n
         S, K, sbm = _sig_inputs(n, sigs, key_idx, "flush_requests")
         out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
@@ -689,6 +708,7 @@ class Verifier:
 
     def flush_replies(self, cols: "ReplyColumns", sigs=None, key_idx=None, digests: bool = True):
         """pbftv_flush_replies: (digests | None, sig_ok | None)."""
+        self._sync_env()
         n = cols.n
         S, K, sbm = _sig_inputs(n, sigs, key_idx, "flush_replies")
         out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
@@ -699,6 +719,7 @@ class Verifier:
                           digests: bool = True, req_digests: bool = False):
         """pbftv_flush_preprepares: (digests | None, request digests | None, sig_ok | None, msg_ok | None).
         states: (view_ids int64[k], last_seqs int64[k])."""
+        self._sync_env()
         n = cols.n
         S, K, sbm = _sig_inputs(n, sigs, key_idx, "flush_preprepares")
         out_d = np.zeros((max(n, 1), 32), np.uint8) if digests else None
@@ -743,6 +764,7 @@ class Verifier:
         return g.value, q.value, b.value
 
     def verify_batch(self, hashes: np.ndarray, sig_rs: np.ndarray, key_idx: np.ndarray) -> np.ndarray:
+        self._sync_env()
         hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)
         sig_rs = np.ascontiguousarray(sig_rs, np.uint8).reshape(-1, 64)
         key_idx = np.ascontiguousarray(key_idx, np.uint32)
@@ -755,6 +777,7 @@ class Verifier:
 
     def verify_batch_dev(self, dev: int, d_hashes: int, d_sigs: int, d_key_idx: int, n: int, d_bitmap: int,
                          stream: int | None = None):
+        self._sync_env()
         _check(self._L.pbftv_ecdsa_p256_verify_batch_dev(self._h, dev, d_hashes, d_sigs, d_key_idx, n, d_bitmap,
                                                          stream))
 
@@ -771,6 +794,7 @@ class Verifier:
         """A zero-argument callable running pbftv_qc_verify on fixed inputs with every
         argument marshalled once (the per-call cost is then the library's plus one
         ctypes call, as for a cgo caller); returns (accepted, quorum reached)."""
+        self._sync_env()
         hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)
         sig_rs = np.ascontiguousarray(sig_rs, np.uint8).reshape(-1, 64)
         key_idx = np.ascontiguousarray(key_idx, np.uint32)
@@ -789,6 +813,7 @@ class Verifier:
         return call
 
     def qc_verify(self, hashes, sig_rs, key_idx, quorum: int):
+        self._sync_env()
         hashes = np.ascontiguousarray(hashes, np.uint8).reshape(-1, 32)
         sig_rs = np.ascontiguousarray(sig_rs, np.uint8).reshape(-1, 64)
         key_idx = np.ascontiguousarray(key_idx, np.uint32)

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-3 profiles of the final library: the headline bench under rocprofv3
+# Profiles of the current library: the headline bench under rocprofv3
 # --kernel-trace --stats (its HIP-event kernel averages must agree with the
 # trace), then PMC passes (one counter group per pass) over tools/pmc_workload.py.
 set -o pipefail
-OUT=${1:-gpurun_out/r03prof}
+OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
