@@ -241,8 +241,10 @@ def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int, gap
     out["in_library_us_p50"] = float(np.median(stamps[:, 1])) * 1e-3
     out["in_library_handover_us_p50"] = float(np.median(stamps[:, 0])) * 1e-3
     out["in_library_to_lock_us_p50"] = float(np.median(stamps[:, 2] >> np.uint64(32))) * 1e-3
+    out["in_library_slots_in_us_p50"] = float(np.median((stamps[:, 2] >> np.uint64(1)) & np.uint64(0x7FFFFFFF))) * 1e-3
     armed = (stamps[:, 2] & np.uint64(1)) == 1
     out["armed_frac"] = float(armed.mean())
+    armed &= stamps[:, 5] > stamps[:, 3]  # GPU stamps present (PBFTV_QC_STAMPS=1 when armed)
     if armed.any():
         a = stamps[armed].astype(np.float64)
         wall = (a[:, 5] - a[:, 3]) / (a[:, 7] * 1e3)

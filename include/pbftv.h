@@ -118,12 +118,19 @@ int pbftv_reset_kernel_times(pbftv_ctx* ctx);
 /* Diagnostics of the last latency-path call (n <= 2048) on device dev:
  * out[0] = host ns from entry to the request being handed over (bell rung or
  * kernel launched), out[1] = host ns from entry to return, out[2] bit 0 = 1
- * if an armed kernel served it, 0 if a launch did, out[2] >> 32 = host ns from
- * entry to holding the device lock, out[3..6] = the armed kernel's
+ * if an armed kernel served it, 0 if a launch did, bits 1..31 = host ns from
+ * entry to the verdicts of the first 8 signatures all in, bits 32..63 = host
+ * ns from entry to holding the device lock, out[3..6] = the armed kernel's
  * slot-0 wave: GPU wall clock and shader clock when it saw the request, and
- * when it wrote its verdict (0 after a launch), out[7] = the wall-clock rate
- * in kHz. */
+ * when it wrote its verdict (0 after a launch; written only while
+ * PBFTV_QC_STAMPS=1 was set when the kernel was armed), out[7] = the
+ * wall-clock rate in kHz. */
 int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]);
+/* The same GPU stamps for every armed wave of the last call (up to `waves`
+ * entries of {seen wall, seen shader clock, done wall, done shader clock};
+ * helper waves past the 8 slots included): returns the number written, 0 if a
+ * launch served the call.  Stamps of waves that had no signature are stale. */
+int pbftv_qc_stamps_all(pbftv_ctx* ctx, int dev, uint64_t* out, uint32_t waves);
 
 /* ---- SHA-256 digests (utils.Hash) ------------------------------------ */
 

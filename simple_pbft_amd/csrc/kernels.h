@@ -123,16 +123,20 @@ uint64_t wave_path_max();
 struct QcMail {
   uint32_t bell, n, stop, expired, cap, halt, live, pad[9];
   static constexpr uint32_t kQcSlots = 8;
+  static constexpr uint32_t kQcCap = 128;  // signatures per call up to which the mailbox is laid out at cap = 128
   static constexpr size_t slot_off(uint32_t i) { return 64 + 192 * (size_t)i; }
-  static constexpr size_t arrays_off() { return 64 + 192 * (size_t)kQcSlots; }
+  static constexpr size_t arrays_off() { return 64 + 192 * (size_t)kQcSlots + 4 * (size_t)kQcCap; }
   static constexpr size_t hashes_off() { return arrays_off(); }
   static constexpr size_t sigs_off(uint32_t cap) { return arrays_off() + 32 * (size_t)cap; }
   static constexpr size_t keys_off(uint32_t cap) { return arrays_off() + 96 * (size_t)cap; }
   static constexpr size_t res_off(uint32_t cap) { return arrays_off() + 100 * (size_t)cap; }
-  // diagnostics: per slot, the armed wave's {wall clock, shader clock} when it
-  // saw its request and when it wrote its verdict (pbftv_qc_stamps)
+  // diagnostics: per armed wave (slots and helpers), its {wall clock, shader
+  // clock} when it saw its request and when it wrote its verdict (pbftv_qc_stamps)
   static constexpr size_t stamps_off(uint32_t cap) { return (res_off(cap) + cap + 63) & ~(size_t)63; }
-  static constexpr size_t bytes(uint32_t cap) { return stamps_off(cap) + 32 * (size_t)kQcSlots + 64; }
+  // each armed wave's first request number once it is resident (4 B per wave),
+  // right after the header's slots region and before the arrays: fixed offset
+  static constexpr size_t bytes(uint32_t cap) { return stamps_off(cap) + 32 * (size_t)kQcCap + 64; }
+  static constexpr size_t live_off() { return 64 + 192 * (size_t)kQcSlots; }
 };
 struct ArmArgs {
   QcMail* mail;
@@ -144,6 +148,8 @@ struct ArmArgs {
   const uint32_t* const* qtabs;
   uint32_t spin;       // between polls: 0 = s_sleep, 1 = none, k >= 2 = k dependent VALU ops
   uint32_t halt;       // the mailbox's halt word at arming: any other value cancels
+  uint64_t* relay;     // wide kernel (kQcCap waves): device word {number, n}, zeroed before launch; null: narrow
+  uint32_t stamps;     // 1: each serving wave writes its GPU timestamps (pbftv_qc_stamps*; PBFTV_QC_STAMPS=1)
 };
 hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st);
 

@@ -111,6 +111,7 @@ int current_gpu() {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = 0;  // hipExtMallocWithFlags flags (0: plain hipMalloc)
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) {
@@ -120,7 +121,7 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 4096);
-    hipError_t e = hipMalloc(&p, want);
+    hipError_t e = flags ? hipExtMallocWithFlags(&p, want, flags) : hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -220,6 +221,12 @@ struct Device {
   int arm_stream = 1;                      // qstream index of the armed kernel
   uint32_t armed_first = 0;                // the armed kernel's first number (its `live` report)
   uint32_t retiring = 0;                   // a rotated-out kernel still waiting for arm_seq's to start
+  uint32_t arm_waves = 0;                  // waves of the armed kernel: kQcSlots (narrow) or kQcCap (wide)
+  DevBuf qrelay;                           // the wide kernels' relay words, one 64-B line per qstream:
+                                           // uncached device memory (read and written past the 8 XCDs' L2s, so
+                                           // no cache maintenance: an agent-scope acquire per poll would
+                                           // invalidate the poller's whole L2)
+  std::chrono::steady_clock::time_point last_wide{};  // the last latency-path call of 9..kQcCap signatures
   bool mail_registered = false;  // the mailbox is in the arm registry
   std::chrono::steady_clock::time_point armed_at{}, last_qc{};
   std::thread keeper;  // qc_keeper_loop
@@ -227,7 +234,7 @@ struct Device {
   bool keeper_stop = false, keeper_idle = false;
   uint64_t rotations = 0;
   // diagnostics of the last latency-path call (pbftv_qc_stamps)
-  uint64_t qc_ns_entry = 0, qc_ns_handover = 0, qc_ns_total = 0;
+  uint64_t qc_ns_entry = 0, qc_ns_handover = 0, qc_ns_total = 0, qc_ns_slots = 0;
   bool qc_armed_served = false;
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
@@ -344,7 +351,7 @@ hipError_t collect_times(Device& d) {
 // ---- the armed latency kernel (verify_kernels.h k_ecdsa_wave_armed) ----
 using pbftv::ArmArgs;
 using pbftv::QcMail;
-constexpr uint32_t kQcCap = 128;  // signatures per latency-path call (mailbox capacity, armed waves)
+constexpr uint32_t kQcCap = QcMail::kQcCap;  // signatures per call the mailbox holds at its usual layout (= wide waves)
 
 bool qc_arm_enabled() {
   const char* e = getenv("PBFTV_QC_ARM");
@@ -429,6 +436,17 @@ hipError_t qc_disarm(Device& d) {
 
 void qc_keeper_loop(Device* d);
 
+// arm the wide kernel (kQcCap waves) while calls of 9..kQcCap signatures keep
+// coming (PBFTV_QC_KEEP_MS since the last one; PBFTV_QC_WIDE=0: never).  Its
+// 120 helper waves hold ~half a SIMD of registers each while armed, so a
+// context that only sees small certificates keeps the narrow kernel.
+bool qc_wide_wanted(const Device& d) {
+  const char* e = getenv("PBFTV_QC_WIDE");
+  if (e && e[0] == '0') return false;
+  if (d.last_wide.time_since_epoch().count() == 0) return false;
+  return std::chrono::steady_clock::now() - d.last_wide < std::chrono::microseconds((int64_t)(qc_keep_ms() * 1000.0));
+}
+
 // Launch the kernel that will serve the next latency-path request (none while
 // a quiesce of this GPU is in progress: the request then takes a launch).
 hipError_t qc_arm(Device& d) {
@@ -448,10 +466,19 @@ hipError_t qc_arm(Device& d) {
   if (++d.seq_counter == 0) d.seq_counter = 1;  // 0 means "none armed"
   const uint32_t want = d.seq_counter;
   const int slot = d.arm_stream ^ 1;  // not behind the previous armed kernel (a rotation overlaps the two)
+  uint64_t* relay = nullptr;
+  if (qc_wide_wanted(d)) {  // certificates of 9..kQcCap signatures were seen lately: helpers for them
+    d.qrelay.flags = hipDeviceMallocUncached;
+    HIP_TRY_E(d.qrelay.ensure(128));
+    relay = reinterpret_cast<uint64_t*>(d.qrelay.as<uint8_t>() + 64 * slot);
+    HIP_TRY_E(hipMemsetAsync(relay, 0, 8, d.qstream[slot]));  // after that stream's previous kernel left
+  }
+  const char* se = getenv("PBFTV_QC_STAMPS");
   const ArmArgs a{qc_mail(d), want, qc_arm_budget(d.id), d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
-                  d.qptrs.as<const uint32_t* const>(), qc_spin(), halt};
+                  d.qptrs.as<const uint32_t* const>(), qc_spin(), halt, relay, se && se[0] == '1' ? 1u : 0u};
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = d.armed_first = want;
+  d.arm_waves = relay ? kQcCap : QcMail::kQcSlots;
   d.arm_stream = slot;
   d.armed_at = std::chrono::steady_clock::now();
   if (!d.keeper.joinable() && qc_keep_ms() > 0) d.keeper = std::thread(qc_keeper_loop, &d);
@@ -482,7 +509,9 @@ hipError_t qc_rotate(Device& d) {
 // retire the rotated-out kernel once its successor is resident
 void qc_retire(Device& d) {
   if (!d.retiring || !d.arm_seq) return;
-  if (__atomic_load_n(&qc_mail(d)->live, __ATOMIC_ACQUIRE) != d.armed_first) return;
+  const uint32_t* live = reinterpret_cast<const uint32_t*>(d.stage.as<uint8_t>() + QcMail::live_off());
+  for (uint32_t w = 0; w < d.arm_waves; ++w)
+    if (__atomic_load_n(live + w, __ATOMIC_ACQUIRE) != d.armed_first) return;  // not every wave resident yet
   __atomic_store_n(&qc_mail(d)->stop, d.retiring, __ATOMIC_RELEASE);
   d.retiring = 0;
 }
@@ -502,7 +531,8 @@ void qc_keeper_loop(Device* d) {
     qc_retire(*d);
     if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
       // also re-arms after a disarm (key change) or a halt (quiesce)
-      if (d->arm_seq == 0 || now >= d->armed_at + half) {
+      const bool reshape = d->arm_seq && (d->arm_waves == kQcCap) != qc_wide_wanted(*d);
+      if (d->arm_seq == 0 || now >= d->armed_at + half || reshape) {
         if (qc_rotate(*d) != hipSuccess) (void)hipGetLastError();  // a call will launch instead
         ++d->rotations;
       }
@@ -1573,7 +1603,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       return hipSetDevice(d.id);
     };
     const bool small = n <= kQcCap;
-    const uint32_t cap = small ? kQcCap : (uint32_t)n;
+    const uint32_t cap = small ? kQcCap : (uint32_t)n;  // the armed kernels assume kQcCap (QcMail::kQcCap)
     if (!small || d.stage.cap < QcMail::bytes(cap) || !d.mail_registered) {
       HIP_TRY(set_dev());
       HIP_TRY(qc_disarm(d));  // (the mailbox is relaid out for n)
@@ -1606,8 +1636,17 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       HIP_TRY(qc_disarm(d));
     }
     uint32_t cur = 0;  // the armed request number serving this call
-    if (n <= QcMail::kQcSlots && d.arm_seq) {
+    if (n > QcMail::kQcSlots && small) d.last_wide = h_in;
+    if (d.arm_seq && n <= d.arm_waves) {
       cur = d.arm_seq;
+      if (n > QcMail::kQcSlots) {  // the helpers' inputs (slots kQcSlots..n-1), before any slot tag
+        std::memcpy(st8 + QcMail::hashes_off() + 32 * QcMail::kQcSlots, hashes + 32 * QcMail::kQcSlots,
+                    32 * (n - QcMail::kQcSlots));
+        std::memcpy(st8 + QcMail::sigs_off(cap) + 64 * QcMail::kQcSlots, sig_rs + 64 * QcMail::kQcSlots,
+                    64 * (n - QcMail::kQcSlots));
+        std::memcpy(st8 + QcMail::keys_off(cap) + 4 * QcMail::kQcSlots, key_idx + QcMail::kQcSlots,
+                    4 * (n - QcMail::kQcSlots));
+      }
       // the kernel waits for cur + 1 next (0 is "none": cancel it at the wrap)
       d.arm_seq = d.seq_counter = cur + 1;
       // the slots: each line's data, then its tags (a line is read by the GPU
@@ -1632,19 +1671,25 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       }
       __atomic_store_n(&m->bell, cur, __ATOMIC_RELEASE);  // inputs and n are in: ring
     } else {
-      // a batch the armed kernel cannot take (n > its slots) leaves it armed
-      // for the next small one
+      // a batch the armed kernel cannot take (n > its waves) leaves it armed
+      // for the next small one; a narrow one is replaced by a wide one for the
+      // next certificate of this size (qc_wide_wanted)
       int rc = launch_plain();
       if (rc != PBFTV_OK) return rc;
-      if (small) HIP_TRY(qc_arm(d));  // the next call's server (no-op while one is armed)
+      if (small) {
+        if (d.arm_seq && n > d.arm_waves && qc_wide_wanted(d)) HIP_TRY(qc_rotate(d));
+        HIP_TRY(qc_arm(d));  // the next call's server (no-op while one is armed)
+      }
     }
     const auto h_bell = std::chrono::steady_clock::now();
     // every wave writes its byte after its last read of the inputs, so once
     // all n bytes are in, the mailbox is free for the next call
     auto t0 = std::chrono::steady_clock::now();
+    const uint64_t slots_n = std::min<uint64_t>(n, QcMail::kQcSlots);
+    auto h_slots = h_bell;
     for (uint64_t next = 0; next < n;) {
       if (res[next] != 0xFF) {
-        ++next;
+        if (++next == slots_n) h_slots = std::chrono::steady_clock::now();
         continue;
       }
       if (cur && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == cur) {
@@ -1690,6 +1735,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(x).count();
     };
     d.qc_ns_entry = ns(h_in - h_entry);
+    d.qc_ns_slots = ns(h_slots - h_entry);
     d.qc_ns_handover = ns(h_bell - h_entry);
     d.qc_ns_total = ns(h_out - h_entry);
     d.qc_armed_served = cur != 0;
@@ -1710,7 +1756,8 @@ int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]) {
   std::memset(out, 0, 8 * sizeof(uint64_t));
   out[0] = d->qc_ns_handover;
   out[1] = d->qc_ns_total;
-  out[2] = (d->qc_armed_served ? 1 : 0) | (std::min<uint64_t>(d->qc_ns_entry, 0xFFFFFFFFull) << 32);
+  out[2] = (d->qc_armed_served ? 1 : 0) | (std::min<uint64_t>(d->qc_ns_slots, 0x7FFFFFFFull) << 1) |
+           (std::min<uint64_t>(d->qc_ns_entry, 0xFFFFFFFFull) << 32);
   if (d->qc_armed_served && d->stage.p) {
     const volatile uint64_t* st = reinterpret_cast<const volatile uint64_t*>(
         d->stage.as<uint8_t>() + QcMail::stamps_off(qc_mail(*d)->cap));
@@ -1720,6 +1767,19 @@ int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]) {
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d->id);
   out[7] = (uint64_t)khz;
   return PBFTV_OK;
+}
+
+int pbftv_qc_stamps_all(pbftv_ctx* ctx, int dev, uint64_t* out, uint32_t waves) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || (waves && !out)) return fail(PBFTV_EINVAL, "bad context, device index or out pointer");
+  std::lock_guard<std::mutex> lk(d->mu);
+  std::memset(out, 0, 4 * sizeof(uint64_t) * waves);
+  if (!d->qc_armed_served || !d->stage.p) return 0;
+  const volatile uint64_t* st = reinterpret_cast<const volatile uint64_t*>(
+      d->stage.as<uint8_t>() + QcMail::stamps_off(qc_mail(*d)->cap));
+  const uint32_t w = std::min(waves, kQcCap);
+  for (uint32_t i = 0; i < 4 * w; ++i) out[i] = st[i];
+  return (int)w;
 }
 
 int pbftv_qc_verify(pbftv_ctx* ctx, const uint8_t* hashes, const uint8_t* sig_rs, const uint32_t* key_idx, uint64_t n,

@@ -11,6 +11,8 @@
 // lanes of a wave run the same number of blocks.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace pbftv {
@@ -224,7 +226,13 @@ hipError_t launch_sha256(const uint8_t* data, const uint64_t* offsets, const uin
     if (e != hipSuccess) return e;
   }
   const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)blocks), dim3(256), 0, st, data, offsets, lengths, order, n, digests,
+  // experiment knob: dynamic LDS per block caps the blocks per CU (occupancy
+  // A/B of the L2 footprint: lanes x the 128-B line each one has open)
+  static const uint32_t pad = [] {
+    const char* e = getenv("PBFTV_SHA_LDS_PAD");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)blocks), dim3(256), pad, st, data, offsets, lengths, order, n, digests,
                      expected, reinterpret_cast<uint32_t*>(bitmap));
   return hipGetLastError();
 }

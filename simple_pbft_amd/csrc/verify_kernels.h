@@ -299,7 +299,10 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
     j0 = 0;
   }
   const int jend = fuse ? S::nD - 1 : S::nD;
-#pragma unroll 1
+#ifndef PBFTV_COMB_UNROLL
+#define PBFTV_COMB_UNROLL 1
+#endif
+#pragma unroll PBFTV_COMB_UNROLL
   for (int j = j0; j < jend; ++j) {
     uint32_t w16[16];
     read_entry_lds(sent, t, w16);
@@ -383,7 +386,7 @@ __device__ __forceinline__ void wave_sum_lanes(jac& P, bool& inf, const uint32_t
                                                const uint4* __restrict__ gtab, const uint4* __restrict__ qtab) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
   constexpr int nW = nG > nQ ? nG : nQ;
-  const int j = threadIdx.x;
+  const int j = (int)(threadIdx.x & 63u);  // (the armed kernel runs four waves per workgroup)
   digit_stream<WG> s1;
   digit_stream<WQ> s2;
   PBFTV_UNROLL for (int k = 0; k < 8; ++k) { s1.w[k] = u1[k]; s2.w[k] = u2[k]; }
@@ -608,7 +611,7 @@ __device__ __forceinline__ bool wave_verify_quads(bool& exc, const uint32_t u1[8
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin;
   constexpr int nW = nG > nQ ? nG : nQ;
   static_assert(nW > 8 && nW <= 16, "one quad per window, four butterfly levels");
-  const int role = threadIdx.x & 3, q = threadIdx.x >> 2;
+  const int role = (int)(threadIdx.x & 3u), q = (int)((threadIdx.x & 63u) >> 2);
   const int d1 = lane_window_digit<WG>(u1, q), d2 = lane_window_digit<WQ>(u2, q);
   uint4 eg[4], eq[4];
   uint32_t w16[16];
@@ -1183,20 +1186,98 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
 // ArmArgs); host words are read with system-scope loads; nothing is written
 // through the scalar cache.  The key tables' pointers and validity flags of
 // the first 128 keys are loaded once, at launch (a key change cancels first).
+// key data of key k: from the per-lane prefetch for k < 128, else from memory
+__device__ __forceinline__ void armed_key(uint32_t k, uint32_t nkeys, const uint4* qt_lo, const uint4* qt_hi,
+                                          uint32_t kv_lo, uint32_t kv_hi, const uint32_t* __restrict__ key_valid,
+                                          const uint4* const* __restrict__ qtabs, bool& key_ok, const uint4*& qtab) {
+  if (k < 128 && k < nkeys) {  // prefetched
+    const int kl = (int)(k & 63);
+    const uint64_t ql = (uint64_t)(uintptr_t)(k < 64 ? qt_lo : qt_hi);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ql, kl),
+                   hi = __builtin_amdgcn_readlane((uint32_t)(ql >> 32), kl);
+    qtab = reinterpret_cast<const uint4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+    key_ok = __builtin_amdgcn_readlane(k < 64 ? kv_lo : kv_hi, kl) != 0;
+  } else {
+    key_ok = k < nkeys && key_valid[k] != 0;
+    qtab = qtabs[k < nkeys ? k : 0];
+  }
+}
+
+// Launched with kQcSlots waves (narrow) or kQcCap waves (wide: certificates
+// of up to 128 signatures, e.g. a 67-vote QC of an n = 100 committee).  Waves
+// past the slots are HELPERS: they never poll host memory; wave 0 relays each
+// request's number and n to them through a word of uncached device memory
+// (`relay`: {number, n}, n = ~0 when wave 0 leaves), and a helper whose index is below n
+// reads its signature from the mailbox arrays (one PCIe round trip; the host
+// writes them before the slot tags) and writes its verdict byte.
 template <int WG, int WQ>
-__global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ mail, uint32_t want, uint64_t budget,
-                                                         const uint32_t* __restrict__ key_valid, uint32_t nkeys,
-                                                         const uint4* __restrict__ gtab,
-                                                         const uint4* const* __restrict__ qtabs, uint32_t spin,
-                                                         uint32_t halt) {
-  const uint32_t b = blockIdx.x, lane = threadIdx.x;
-  const uint64_t t0 = wall_clock64();
-  if (b == 0 && lane == 0) reinterpret_cast<volatile uint32_t*>(mail)[6] = want;  // live: resident now
-  // key data for keys < 128, two per lane (lane l: keys l and l + 64)
-  const uint4* qt_lo = lane < nkeys ? qtabs[lane] : nullptr;
-  const uint4* qt_hi = lane + 64 < nkeys ? qtabs[lane + 64] : nullptr;
-  const uint32_t kv_lo = lane < nkeys ? key_valid[lane] : 0u, kv_hi = lane + 64 < nkeys ? key_valid[lane + 64] : 0u;
+__global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
+  // four waves per workgroup: one CU takes a workgroup's waves on its four
+  // SIMDs, so no two armed waves of a workgroup share a SIMD's issue slots
+  const uint32_t b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  QcMail* const mail = a.mail;
   uint8_t* const base = reinterpret_cast<uint8_t*>(mail);
+  uint32_t want = a.want;
+  const uint64_t t0 = wall_clock64();
+  // live: this wave is resident (a rotation retires the old kernel after all are)
+  if (lane == 0) reinterpret_cast<volatile uint32_t*>(base + QcMail::live_off())[b] = want;
+  // key data for keys < 128, two per lane (lane l: keys l and l + 64)
+  const uint32_t nkeys = a.nkeys;
+  const uint4* qt_lo = lane < nkeys ? reinterpret_cast<const uint4* const*>(a.qtabs)[lane] : nullptr;
+  const uint4* qt_hi = lane + 64 < nkeys ? reinterpret_cast<const uint4* const*>(a.qtabs)[lane + 64] : nullptr;
+  const uint32_t kv_lo = lane < nkeys ? a.key_valid[lane] : 0u, kv_hi = lane + 64 < nkeys ? a.key_valid[lane + 64] : 0u;
+  const uint4* gtab = reinterpret_cast<const uint4*>(a.gtab);
+  const uint4* const* qtabs = reinterpret_cast<const uint4* const*>(a.qtabs);
+  uint64_t* const relay = a.relay;
+  if (b >= QcMail::kQcSlots) {
+    // ---- helper wave ----
+    uint32_t last = 0;  // the relay starts at {0, 0}; request numbers are never 0
+    for (;;) {
+      uint64_t r = 0;
+      for (;;) {
+        // (uncached memory: a relaxed system-scope load sees wave 0's store
+        // with no cache maintenance; the host inputs read next were written
+        // before the slot tags wave 0 saw, and host memory is not cached here)
+        r = __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)r != last || wall_clock64() - t0 > a.budget) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      const uint32_t seq = (uint32_t)r, n = (uint32_t)(r >> 32);
+      if (seq == last || n == 0xFFFFFFFFu) return;  // budget, or wave 0 left
+      last = seq;
+      if (b >= n) continue;
+      const uint64_t seen_wall = wall_clock64(), seen_clk = clock64();
+      __builtin_amdgcn_s_setprio(3);
+      constexpr uint32_t cap = QcMail::kQcCap;  // the armed path's layout (the host relays it out only after a disarm)
+      // lanes 0-7 the hash, 8-23 r || s, 24 the key index: one round trip
+      const uint32_t* src = lane < 8    ? reinterpret_cast<const uint32_t*>(base + QcMail::hashes_off() + 32 * b) + lane
+                            : lane < 24 ? reinterpret_cast<const uint32_t*>(base + QcMail::sigs_off(cap) + 64 * b) + (lane - 8)
+                                        : reinterpret_cast<const uint32_t*>(base + QcMail::keys_off(cap) + 4 * b);
+      const uint32_t v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t e[8], rr[8], ss[8];
+      PBFTV_UNROLL for (int t = 0; t < 8; ++t) {
+        e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, t));
+        rr[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 8 + t));
+        ss[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 16 + t));
+      }
+      bool key_ok;
+      const uint4* qtab;
+      armed_key(__builtin_amdgcn_readlane(v, 24), nkeys, qt_lo, qt_hi, kv_lo, kv_hi, a.key_valid, qtabs, key_ok, qtab);
+      const bool ok = wave_verify_words<WG, WQ>(e, rr, ss, key_ok, gtab, qtab);
+      if (lane == 0) {
+        if (a.stamps) {
+          volatile uint64_t* st = reinterpret_cast<volatile uint64_t*>(base + QcMail::stamps_off(cap)) + 4 * b;
+          st[0] = seen_wall;  // diagnostics (pbftv_qc_stamps_all), before the verdict
+          st[1] = seen_clk;
+          st[2] = wall_clock64();
+          st[3] = clock64();
+        }
+        reinterpret_cast<volatile uint8_t*>(base)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  // ---- slot wave ----
   const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b));
   const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
   for (;; ++want) {
@@ -1213,22 +1294,26 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
         serve = true;
         break;
       }
-      if (__builtin_amdgcn_readlane(v, 48 + 2) == want || __builtin_amdgcn_readlane(v, 48 + 5) != halt ||
-          wall_clock64() - t0 > budget)
+      if (__builtin_amdgcn_readlane(v, 48 + 2) == want || __builtin_amdgcn_readlane(v, 48 + 5) != a.halt ||
+          wall_clock64() - t0 > a.budget)
         break;  // header stop / halt, or the budget
-      if (spin == 0) {
+      if (a.spin == 0) {
         __builtin_amdgcn_s_sleep(2);
-      } else if (spin > 1) {
+      } else if (a.spin > 1) {
         uint32_t x = lane;
-        for (uint32_t j = 0; j < spin; ++j) asm volatile("v_mad_u32_u24 %0, %0, %0, %0" : "+v"(x));
+        for (uint32_t j = 0; j < a.spin; ++j) asm volatile("v_mad_u32_u24 %0, %0, %0, %0" : "+v"(x));
       }
     }
     if (!serve) {
+      if (b == 0 && relay && lane == 0)  // the helpers leave with wave 0
+        __hip_atomic_store(relay, ((uint64_t)0xFFFFFFFFu << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (lane == 0) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
     const uint64_t seen_wall = wall_clock64(), seen_clk = clock64();
     const uint32_t n = __builtin_amdgcn_readlane(v, 1);
+    if (b == 0 && relay && n > QcMail::kQcSlots && lane == 0)
+      __hip_atomic_store(relay, ((uint64_t)n << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (b >= n) continue;
     // a certificate's waves go ahead of whatever else shares their SIMDs (the
     // waves of a large batch: issue priority only, nothing is preempted)
@@ -1242,25 +1327,19 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
     }
     bool key_ok;
     const uint4* qtab;
-    if (k < 128 && k < nkeys) {  // prefetched
-      const int kl = (int)(k & 63);
-      const uint64_t ql = (uint64_t)(uintptr_t)(k < 64 ? qt_lo : qt_hi);
-      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ql, kl),
-                     hi = __builtin_amdgcn_readlane((uint32_t)(ql >> 32), kl);
-      qtab = reinterpret_cast<const uint4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
-      key_ok = __builtin_amdgcn_readlane(k < 64 ? kv_lo : kv_hi, kl) != 0;
-    } else {
-      key_ok = k < nkeys && key_valid[k] != 0;
-      qtab = qtabs[k < nkeys ? k : 0];
-    }
+    armed_key(k, nkeys, qt_lo, qt_hi, kv_lo, kv_hi, a.key_valid, qtabs, key_ok, qtab);
     const bool ok = wave_verify_words<WG, WQ>(e, r, s, key_ok, gtab, qtab);
     if (lane == 0) {
-      const uint32_t cap = __hip_atomic_load(&mail->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      volatile uint64_t* st = reinterpret_cast<volatile uint64_t*>(base + QcMail::stamps_off(cap)) + 4 * b;
-      st[0] = seen_wall;  // diagnostics (pbftv_qc_stamps), before the verdict
-      st[1] = seen_clk;
-      st[2] = wall_clock64();
-      st[3] = clock64();
+      // the armed path's layout is always cap = kQcCap (no PCIe round trip for
+      // the header's cap between the verdict and its store)
+      constexpr uint32_t cap = QcMail::kQcCap;
+      if (a.stamps) {
+        volatile uint64_t* st = reinterpret_cast<volatile uint64_t*>(base + QcMail::stamps_off(cap)) + 4 * b;
+        st[0] = seen_wall;  // diagnostics (pbftv_qc_stamps), before the verdict
+        st[1] = seen_clk;
+        st[2] = wall_clock64();
+        st[3] = clock64();
+      }
       // (coherent host memory is not cached on the GPU: the stores leave in
       // order; a system-scope release here would write back the L2 first)
       reinterpret_cast<volatile uint8_t*>(base)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
@@ -1271,9 +1350,8 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave_armed(QcMail* __restrict__ ma
 
 template <int WG, int WQ>
 void launch_armed_w(const ArmArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3(QcMail::kQcSlots), dim3(64), 0, st, a.mail, a.want, a.budget,
-                     a.key_valid, a.nkeys, reinterpret_cast<const uint4*>(a.gtab),
-                     reinterpret_cast<const uint4* const*>(a.qtabs), a.spin, a.halt);
+  hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3((a.relay ? QcMail::kQcCap : QcMail::kQcSlots) / 4), dim3(256), 0,
+                     st, a);
 }
 
 template <int WG, int WQ>

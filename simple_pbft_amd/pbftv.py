@@ -74,6 +74,7 @@ def lib() -> ctypes.CDLL:
         "pbftv_reset_kernel_times": (ctypes.c_int, [_vp]),
         "pbftv_qc_stamps": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
         "pbftv_set_latency_path_max": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+        "pbftv_qc_stamps_all": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_uint32]),
         "pbftv_hash_hex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_char_p]),
         "pbftv_sha256_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
         "pbftv_digest_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
@@ -562,6 +563,13 @@ class Verifier:
     def reset_kernel_times(self):
         _check(self._L.pbftv_reset_kernel_times(self._h))
 
+    def qc_stamps_all(self, n: int, dev: int = 0) -> np.ndarray:
+        """pbftv_qc_stamps_all: (n, 4) uint64 {seen wall, seen clk, done wall, done clk}
+        per armed wave of the last call (zeros after a launch)."""
+        o = np.zeros((n, 4), np.uint64)
+        self._L.pbftv_qc_stamps_all(self._h, dev, o.ctypes.data, n)
+        return o
+
     def qc_stamps(self, dev: int = 0) -> dict:
         """pbftv_qc_stamps: where the last latency-path call's time went (host
         hand-over / total in us; for an armed serve, the GPU's own serve time
@@ -570,7 +578,7 @@ class Verifier:
         _check(self._L.pbftv_qc_stamps(self._h, dev, o.ctypes.data))
         armed = bool(int(o[2]) & 1)
         r = {"handover_us": float(o[0]) * 1e-3, "total_us": float(o[1]) * 1e-3, "armed": armed,
-             "entry_us": float(int(o[2]) >> 32) * 1e-3}
+             "entry_us": float(int(o[2]) >> 32) * 1e-3, "slots_in_us": float((int(o[2]) >> 1) & 0x7FFFFFFF) * 1e-3}
         if armed and o[5] > o[3]:
             wall_s = float(o[5] - o[3]) / (float(o[7]) * 1e3)
             r["gpu_serve_us"] = wall_s * 1e6

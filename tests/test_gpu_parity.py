@@ -527,13 +527,15 @@ def test_armed_latency_path(oracle_lib, mode, monkeypatch):
             o = rng.choice(n_all, n, replace=False)
             got = v.verify_batch(hashes[o], sigs[o], kidx[o])
             assert (got == want[o]).all(), (it, n)
-            if n <= 8 and it > 0:
-                served.append((it, v.qc_stamps(0)["armed"]))
+            if (n <= 8 and it > 0) or (8 < n <= 128 and it > 3):
+                served.append((it, n, v.qc_stamps(0)["armed"]))
             time.sleep(0.06)  # three budgets (keeper) / sixty (expiring)
         if mode == "keeper":
-            assert all(a for _, a in served), served  # the keeper kept one armed through every pause
+            # the keeper kept one armed through every pause -- after the first
+            # 67-signature call a WIDE one (helper waves serve up to 128)
+            assert all(a for _, _, a in served), served
         else:
-            assert not any(a for _, a in served), served  # every one expired: launched instead
+            assert not any(a for _, _, a in served), served  # every one expired: launched instead
         # a key change while a kernel is armed: it is cancelled first
         assert v.set_key(0, keys[0])
         o = rng.choice(n_all, 3, replace=False)

@@ -113,6 +113,37 @@ def part_stamps(ver, quick):
     return out
 
 
+def part_wide(ver, quick):
+    """Where a 67-signature certificate's time goes on the wide armed kernel
+    (pbftv_qc_stamps_all): helper start and finish relative to slot 0 seeing
+    the request, GPU wall-clock us."""
+    calls = fresh_calls(ver, 100, 67, 120, 307)
+    timed_calls(calls[:20], 67)
+    rows = []
+    for call in calls[20:]:
+        t0 = time.perf_counter()
+        acc, ok = call()
+        wall = (time.perf_counter() - t0) * 1e6
+        st = ver.qc_stamps_all(67).astype(np.int64)
+        s0 = ver.qc_stamps(0)
+        if not s0["armed"] or st[0, 0] == 0:
+            continue
+        khz = 100000.0
+        rel_seen = (st[:, 0] - st[0, 0]) / khz * 1e3
+        rel_done = (st[:, 2] - st[0, 0]) / khz * 1e3
+        dur = (st[:, 2] - st[:, 0]) / khz * 1e3
+        rows.append({"wall": wall, "lib": s0["total_us"], "lib_slots_in": s0["slots_in_us"],
+                     "lib_handover": s0["handover_us"], "slot_seen_max": float(rel_seen[:8].max()),
+                     "helper_seen_med": float(np.median(rel_seen[8:])), "helper_seen_max": float(rel_seen[8:].max()),
+                     "slot_done_max": float(rel_done[:8].max()), "helper_done_max": float(rel_done[8:].max()),
+                     "slot_dur_med": float(np.median(dur[:8])), "helper_dur_med": float(np.median(dur[8:])),
+                     "helper_dur_max": float(dur[8:].max())})
+    out = {"calls": len(rows)}
+    for k in (rows[0].keys() if rows else []):
+        out[k + "_p50"] = float(np.median([r[k] for r in rows]))
+    return out
+
+
 def part_free(ver, quick):
     calls = fresh_calls(ver, 4, 3, 8, 7)
     res = {}
@@ -234,7 +265,7 @@ def part_cpu(ver, quick):
     return out
 
 
-PARTS = {"stamps": part_stamps, "b2b": part_b2b, "tick": part_tick, "free": part_free, "load": part_load, "host": part_host,
+PARTS = {"wide": part_wide, "stamps": part_stamps, "b2b": part_b2b, "tick": part_tick, "free": part_free, "load": part_load, "host": part_host,
          "cpu": part_cpu}
 
 
@@ -243,6 +274,8 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--parts", default="cpu,b2b,free,tick,load,host")
     a = ap.parse_args()
+    if os.environ.get("PBFTV_QC_STAMPS") is None and any(p in a.parts for p in ("wide", "stamps")):
+        os.environ["PBFTV_QC_STAMPS"] = "1"  # the armed kernels write their GPU timestamps (diagnostics)
     ver = Verifier(device_mask=1)
     for p in a.parts.split(","):
         t0 = time.perf_counter()
