@@ -1719,7 +1719,9 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         break;
       }
     }
-    if (d.keeper_idle) {  // past its keep window: a call makes it keep the kernel armed again
+    if (d.keeper_idle || (d.arm_seq == 0 && d.keeper.joinable())) {
+      // past its keep window, or nothing armed after a larger call: the
+      // keeper arms one again as soon as this call releases the device
       d.keeper_idle = false;
       d.keeper_cv.notify_one();
     }

@@ -159,6 +159,140 @@ __global__ void __launch_bounds__(256, PBFTV_SHA_WAVES) k_sha256(const uint8_t* 
   }
 }
 
+// ---- line-aligned staging (k_sha256_ring) ----------------------------------
+// k_sha256 reads each block as 17 dword-aligned dwords starting at the
+// message's own alignment, so every 128-B line of a message is fetched by two
+// consecutive block loads one compression apart, and ~20 % of the second
+// fetches miss the L2 (config 5: 24.5M 128-B requests for 2.18 GB of messages,
+// 1.44x, profiles/r04_sha_fetch_calibration.json).  Here each lane fetches its
+// message's ALIGNED 128-B lines, each exactly once (8 dwordx4 loads, issued a
+// compression ahead), and keeps the last two in LDS; a block's 17 dwords are
+// read back at the lane's own dword position.  LDS is ring[pos][thread]
+// (pos = dword of the two-line ring, 0..63, plus a 16-dword mirror of line
+// slot 0 at 64..79 so a 17-dword window never wraps): the address of every
+// access is pos * 1024 + 4 * thread, so a wave's lanes always hit 64 distinct
+// banks whatever their positions.  80 KiB per 256-thread block: two blocks per
+// CU (2 waves/SIMD -- k_sha256 runs no faster at 4, r04_sha_fetch_calibration).
+// A line is 128-B aligned, so it lies in the page of a message byte: reading a
+// whole line never faults where the message is mapped.
+constexpr uint32_t kRingPos = 80;  // 2 x 32 line dwords + the 16-dword mirror
+
+__device__ __forceinline__ void ring_store(uint32_t* ring, uint32_t t, uint32_t line, const uint32_t L[32]) {
+  uint32_t* r = ring + (32u * (line & 1u)) * 256u + t;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) r[k * 256] = L[k];
+  if ((line & 1u) == 0) {
+    uint32_t* mr = ring + 64u * 256u + t;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) mr[k * 256] = L[k];
+  }
+}
+
+__device__ __forceinline__ void line_load(const uint32_t* __restrict__ p, uint32_t L[32]) {
+  const uint4* v = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 x = v[k];
+    L[4 * k] = x.x; L[4 * k + 1] = x.y; L[4 * k + 2] = x.z; L[4 * k + 3] = x.w;
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) k_sha256_ring(const uint8_t* __restrict__ data, const uint64_t* __restrict__ offsets,
+                                                         const uint32_t* __restrict__ lengths,
+                                                         const uint32_t* __restrict__ order, uint64_t n,
+                                                         uint8_t* __restrict__ digests, const uint8_t* __restrict__ expected,
+                                                         uint32_t* __restrict__ bitmap32) {
+  __shared__ uint32_t ring[kRingPos * 256];  // [pos][thread], 80 KiB (static: gfx950 allows up to 160 KiB)
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + t;
+  if (i >= n) return;  // (no barriers: every lane owns its ring column)
+  const uint64_t m = order ? order[i] : i;
+  const uint8_t* base = data + offsets[m];
+  const uint32_t len = lengths[m];
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base);
+  const uint32_t* L0 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)127);
+  const uint32_t lob = (uint32_t)(a & 127u), sh = (uint32_t)(a & 3u);
+  const uint32_t D0 = lob >> 2;                  // the message's first dword in line 0
+  const uint32_t nlines = (lob + len + 127u) >> 7;  // lines holding message bytes (>= 1 for len >= 1)
+  uint32_t L[32];
+  // lines 0 and 1 (blocks 0 and 1 need nothing past line 1)
+  line_load(L0, L);
+  ring_store(ring, t, 0, L);
+  uint32_t R = 1;  // next line to store
+  if (nlines > 1) {
+    line_load(L0 + 32, L);
+    ring_store(ring, t, 1, L);
+    R = 2;
+  }
+  uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  const uint32_t nfull = len >> 6;
+  uint32_t w[16], x[17];
+  for (uint32_t blk = 0; blk < nfull; ++blk) {
+    const uint32_t D = D0 + 16u * blk;  // this block's first dword (line-0 relative)
+    const uint32_t* rp = ring + (D & 63u) * 256u + t;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) x[j] = rp[j * 256];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(x[j + 1], x[j], sh));
+    // the next block's first line f: lines below f are dead; line R goes into
+    // the slot of line R - 2 once that is dead, loaded now and stored after
+    // this compression (one compression of latency hiding)
+    const uint32_t f = (D + 16u) >> 5;
+    const bool fetch = R < nlines && R - 2u < f;
+    if (fetch) line_load(L0 + 32u * R, L);
+    compress(st, w);
+    if (fetch) {
+      ring_store(ring, t, R, L);
+      ++R;
+    }
+  }
+  // tail: rem bytes (0..63) + 0x80 + zeros + 64-bit bit length, in one or two
+  // blocks; ring bytes past the message end are masked off
+  const uint32_t rem = len - (nfull << 6);
+  {
+    const uint32_t D = D0 + 16u * nfull;
+    const uint32_t* rp = ring + (D & 63u) * 256u + t;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) x[j] = rp[j * 256];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t y = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);  // tail bytes 4j..4j+3, little-endian
+    const int v = (int)rem - 4 * j;                                  // message bytes remaining at this word
+    const uint32_t keep = v >= 4 ? 0xFFFFFFFFu : (v <= 0 ? 0u : ((1u << (8 * v)) - 1u));
+    y &= keep;
+    if (v >= 0 && v < 4) y |= 0x80u << (8 * v);
+    w[j] = __builtin_bswap32(y);
+  }
+  const uint64_t bits = (uint64_t)len << 3;
+  if (rem + 9 <= 64) {
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+    compress(st, w);
+  } else {
+    compress(st, w);
+#pragma unroll
+    for (int j = 0; j < 14; ++j) w[j] = 0;
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+    compress(st, w);
+  }
+  uint4* out = reinterpret_cast<uint4*>(digests + 32 * m);
+  const uint4 o0 = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                              __builtin_bswap32(st[3]));
+  const uint4 o1 = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                              __builtin_bswap32(st[7]));
+  out[0] = o0;
+  out[1] = o1;
+  if (expected) {
+    const uint4* ex = reinterpret_cast<const uint4*>(expected + 32 * m);
+    const uint4 e0 = ex[0], e1 = ex[1];
+    const bool eq = e0.x == o0.x && e0.y == o0.y && e0.z == o0.z && e0.w == o0.w && e1.x == o1.x && e1.y == o1.y &&
+                    e1.z == o1.z && e1.w == o1.w;
+    if (eq) atomicOr(bitmap32 + (m >> 5), 1u << (m & 31));
+  }
+}
+
 // ---- block-count bucketing (device counting sort) ----
 constexpr uint32_t kBuckets = 1024;
 
@@ -232,8 +366,17 @@ hipError_t launch_sha256(const uint8_t* data, const uint64_t* offsets, const uin
     const char* e = getenv("PBFTV_SHA_LDS_PAD");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
-  hipLaunchKernelGGL(k_sha256, dim3((uint32_t)blocks), dim3(256), pad, st, data, offsets, lengths, order, n, digests,
-                     expected, reinterpret_cast<uint32_t*>(bitmap));
+  static const bool ring = [] {  // PBFTV_SHA_RING=0: the dword-window kernel (A/B)
+    const char* e = getenv("PBFTV_SHA_RING");
+    return !(e && e[0] == '0');
+  }();
+  if (ring) {
+    hipLaunchKernelGGL(k_sha256_ring, dim3((uint32_t)blocks), dim3(256), 0, st, data, offsets, lengths, order, n,
+                       digests, expected, reinterpret_cast<uint32_t*>(bitmap));
+  } else {
+    hipLaunchKernelGGL(k_sha256, dim3((uint32_t)blocks), dim3(256), pad, st, data, offsets, lengths, order, n,
+                       digests, expected, reinterpret_cast<uint32_t*>(bitmap));
+  }
   return hipGetLastError();
 }
 
