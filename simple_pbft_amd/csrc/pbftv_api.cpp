@@ -1579,6 +1579,20 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
   const auto h_entry = std::chrono::steady_clock::now();
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
   if (n && (!hashes || !sig_rs || !key_idx || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
+  if (n && n <= QcMail::kQcSlots && !ctx->devs.empty()) {
+    // A certificate after an idle second finds this core's caches cold (the
+    // caller slept; its core's private caches were flushed): start the misses
+    // of the lines the armed path touches now, in parallel, instead of one
+    // after another (device lock and state, the mailbox header, slot lines and
+    // result bytes).  A stale mailbox pointer is harmless: a prefetch never faults.
+    const Device* d0 = ctx->devs[0].get();
+    __builtin_prefetch(&d0->mu, 1, 3);
+    __builtin_prefetch(&d0->arm_seq, 1, 3);
+    if (const uint8_t* mb = static_cast<const uint8_t*>(d0->stage.p)) {
+      for (size_t off = 0; off < QcMail::arrays_off(); off += 64) __builtin_prefetch(mb + off, 1, 3);
+      __builtin_prefetch(mb + QcMail::res_off(QcMail::kQcCap), 1, 3);
+    }
+  }
   for (auto& dp : ctx->devs)
     if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
   if (n && n <= ctx->wave_max.load(std::memory_order_relaxed)) {

@@ -50,7 +50,7 @@ def fresh_calls(ver, n_keys, sigs, count, seed, register=True):
                                    K[c * sigs:(c + 1) * sigs], quorum=sigs) for c in range(count)]
 
 
-def timed_calls(calls, sigs, gap_s=0.0):
+def timed_calls(calls, sigs, gap_s=0.0, ver=None, serve=None):
     ts = []
     for call in calls:
         if gap_s:
@@ -59,6 +59,10 @@ def timed_calls(calls, sigs, gap_s=0.0):
         acc, ok = call()
         ts.append(time.perf_counter() - t0)
         assert ok and acc == sigs, (acc, sigs)
+        if serve is not None:  # the armed slot-0 wave's GPU serve time (PBFTV_QC_STAMPS=1)
+            st = ver.qc_stamps(0)
+            if "gpu_serve_us" in st:
+                serve.append(st["gpu_serve_us"])
     return ts
 
 
@@ -172,9 +176,12 @@ def part_load(ver, quick):
     db = ver.alloc(0, n // 8 + 1)
     out = {}
     timed_calls(calls[:20], 3)
-    out["idle_3sigs_gap2ms"] = pct(timed_calls(calls[20:320], 3, 0.002))
+    si3, si67 = [], []
+    out["idle_3sigs_gap2ms"] = pct(timed_calls(calls[20:320], 3, 0.002, ver, si3))
     timed_calls(calls67[:10], 67)
-    out["idle_67sigs_gap2ms"] = pct(timed_calls(calls67[10:110], 67, 0.002))
+    out["idle_67sigs_gap2ms"] = pct(timed_calls(calls67[10:110], 67, 0.002, ver, si67))
+    out["idle_gpu_serve_us_p50"] = {"3sigs": float(np.median(si3)) if si3 else None,
+                                    "67sigs": float(np.median(si67)) if si67 else None}
     stop = threading.Event()
     done = [0]
 
@@ -188,8 +195,11 @@ def part_load(ver, quick):
     th.start()
     time.sleep(0.05)
     t0 = time.perf_counter()
-    out["loaded_3sigs_gap2ms"] = pct(timed_calls(calls[320:620], 3, 0.002))
-    out["loaded_67sigs_gap2ms"] = pct(timed_calls(calls67[110:220], 67, 0.002))
+    sv3, sv67 = [], []
+    out["loaded_3sigs_gap2ms"] = pct(timed_calls(calls[320:620], 3, 0.002, ver, sv3))
+    out["loaded_67sigs_gap2ms"] = pct(timed_calls(calls67[110:220], 67, 0.002, ver, sv67))
+    out["loaded_gpu_serve_us_p50"] = {"3sigs": float(np.median(sv3)) if sv3 else None,
+                                      "67sigs": float(np.median(sv67)) if sv67 else None}
     dt = time.perf_counter() - t0
     b0 = done[0]
     stop.set()
@@ -274,7 +284,7 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--parts", default="cpu,b2b,free,tick,load,host")
     a = ap.parse_args()
-    if os.environ.get("PBFTV_QC_STAMPS") is None and any(p in a.parts for p in ("wide", "stamps")):
+    if os.environ.get("PBFTV_QC_STAMPS") is None and any(p in a.parts for p in ("wide", "stamps", "load")):
         os.environ["PBFTV_QC_STAMPS"] = "1"  # the armed kernels write their GPU timestamps (diagnostics)
     ver = Verifier(device_mask=1)
     for p in a.parts.split(","):
