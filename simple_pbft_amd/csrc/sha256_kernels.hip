@@ -215,10 +215,15 @@ __global__ void __launch_bounds__(256, 2) k_sha256_ring(const uint8_t* __restric
   const uint32_t D0 = lob >> 2;                  // the message's first dword in line 0
   const uint32_t nlines = (lob + len + 127u) >> 7;  // lines holding message bytes (>= 1 for len >= 1)
   uint32_t L[32];
-  // lines 0 and 1 (blocks 0 and 1 need nothing past line 1)
-  line_load(L0, L);
-  ring_store(ring, t, 0, L);
-  uint32_t R = 1;  // next line to store
+  // lines 0 and 1 (blocks 0 and 1 need nothing past line 1).  An empty message
+  // on a line boundary has no line (it may sit at the very end of a mapping):
+  // nothing is read, and the tail masks every ring byte.
+  uint32_t R = 0;  // next line to store
+  if (nlines > 0) {
+    line_load(L0, L);
+    ring_store(ring, t, 0, L);
+    R = 1;
+  }
   if (nlines > 1) {
     line_load(L0 + 32, L);
     ring_store(ring, t, 1, L);
