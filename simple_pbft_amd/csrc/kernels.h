@@ -125,18 +125,25 @@ struct QcMail {
   static constexpr uint32_t kQcSlots = 8;
   static constexpr uint32_t kQcCap = 128;  // signatures per call up to which the mailbox is laid out at cap = 128
   static constexpr size_t slot_off(uint32_t i) { return 64 + 192 * (size_t)i; }
-  static constexpr size_t arrays_off() { return 64 + 192 * (size_t)kQcSlots + 4 * (size_t)kQcCap; }
-  static constexpr size_t hashes_off() { return arrays_off(); }
-  static constexpr size_t sigs_off(uint32_t cap) { return arrays_off() + 32 * (size_t)cap; }
-  static constexpr size_t keys_off(uint32_t cap) { return arrays_off() + 96 * (size_t)cap; }
-  static constexpr size_t res_off(uint32_t cap) { return arrays_off() + 100 * (size_t)cap; }
+  // each armed wave's first request number once it is resident (4 B per wave)
+  static constexpr size_t live_off() { return 64 + 192 * (size_t)kQcSlots; }
+  // one verdict byte per signature, right after the live words: with the
+  // header and the slot lines in the mailbox's FIRST 4-KiB page, so a
+  // certificate of <= kQcSlots touches one page of it (one TLB entry on the
+  // host, one translation on the GPU, both warm from the polling)
+  static constexpr size_t res_off(uint32_t = kQcCap) { return live_off() + 4 * (size_t)kQcCap; }
+  // the input arrays of signatures kQcSlots.. (and of every signature on the
+  // launched path), after cap verdict bytes
+  static constexpr size_t arrays_off(uint32_t cap = kQcCap) {
+    return (res_off() + (cap > kQcCap ? cap : kQcCap) + 63) & ~(size_t)63;
+  }
+  static constexpr size_t hashes_off(uint32_t cap = kQcCap) { return arrays_off(cap); }
+  static constexpr size_t sigs_off(uint32_t cap) { return arrays_off(cap) + 32 * (size_t)cap; }
+  static constexpr size_t keys_off(uint32_t cap) { return arrays_off(cap) + 96 * (size_t)cap; }
   // diagnostics: per armed wave (slots and helpers), its {wall clock, shader
   // clock} when it saw its request and when it wrote its verdict (pbftv_qc_stamps)
-  static constexpr size_t stamps_off(uint32_t cap) { return (res_off(cap) + cap + 63) & ~(size_t)63; }
-  // each armed wave's first request number once it is resident (4 B per wave),
-  // right after the header's slots region and before the arrays: fixed offset
+  static constexpr size_t stamps_off(uint32_t cap) { return (keys_off(cap) + 4 * (size_t)cap + 63) & ~(size_t)63; }
   static constexpr size_t bytes(uint32_t cap) { return stamps_off(cap) + 32 * (size_t)kQcCap + 64; }
-  static constexpr size_t live_off() { return 64 + 192 * (size_t)kQcSlots; }
 };
 struct ArmArgs {
   QcMail* mail;

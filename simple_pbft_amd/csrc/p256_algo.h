@@ -514,6 +514,33 @@ struct CombSteps {
   PBFTV_HDM static constexpr int win(int j) { return j < 2 * nMin ? j >> 1 : j - nMin; }
 };
 
+// (a & b) ^ c: ONE v_bitop3_b32 on the device (truth table 0x6A: bit
+// 4 a + 2 b + c of the table is the result)
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t and_xor(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x6A);
+}
+#else
+static inline uint32_t and_xor(uint32_t a, uint32_t b, uint32_t c) { return (a & b) ^ c; }
+#endif
+
+// entry_to_fe, then y = neg ? -y : y (D-type), with the negation folded into
+// the unpacking: a limb of y is (bits & mask ^ m) - m, two instructions
+// instead of entry_to_fe's mask plus fs_cneg's negate and select
+PBFTV_HD void entry_to_fe_cneg(fe& x, fe& y, const uint32_t e[16], bool neg) {
+  fe_from_words(x, e);
+  const uint32_t* w = e + 8;
+  const uint32_t m = 0u - (uint32_t)neg;
+  y.v[0] = and_xor(w[0], kMask29, m) - m;
+  PBFTV_UNROLL for (int i = 1; i < 8; ++i) {
+    const int bit = 29 * i, wi = bit >> 5, sh = bit & 31;
+    const uint32_t lo = w[wi] >> sh;
+    const uint32_t hi = (sh && wi + 1 < 8) ? (w[wi + 1] << (32 - sh)) : 0u;
+    y.v[i] = and_xor(lo | hi, kMask29, m) - m;
+  }
+  y.v[8] = ((w[7] >> 8) ^ m) - m;
+}
+
 // The accumulator is XYZZ on signed limbs with W = sigma Y (neg_y: sigma = -1;
 // xyzz_madd_s_flip).  Per signature:
 //   * the first two digits both non-zero (all but ~2^-20 of signatures): the
@@ -535,8 +562,7 @@ PBFTV_HD void comb_first2_s(xyzz_s& acc, bool& neg_y, int d0, const uint32_t w0[
 PBFTV_HD void comb_step_s(xyzz_s& acc, bool& inf, bool& neg_y, int d, const uint32_t w[16]) {
   if (d == 0) return;
   fe x, y;
-  entry_to_fe(x, y, w);
-  fs_cneg(y, y, (d < 0) != neg_y);  // sigma * (+-y): D-type (no carry chain)
+  entry_to_fe_cneg(x, y, w, (d < 0) != neg_y);  // sigma * (+-y): D-type (no carry chain)
   if (inf) {
     acc.x = x;
     fs_norm(acc.y, y);

@@ -197,6 +197,27 @@ struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // ---- what a latency-path call reads and writes, together from here to
+  // hot_end (prefetched at its entry: a certificate after an idle second finds
+  // them cold, and one line per miss would serialise behind the lock) ----
+  bool have_keys = false;
+  bool mail_registered = false;  // the mailbox is in the arm registry
+  bool keeper_stop = false, keeper_idle = false;
+  bool qc_armed_served = false;
+  HostBuf stage;  // zero-copy inputs/outputs of the small-batch path (a QcMail mailbox)
+  // the armed latency kernel (k_ecdsa_wave_armed): a persistent server that
+  // waits for the next request's doorbell in `stage`; arm_seq = the request
+  // number it waits for (0: none armed)
+  uint32_t arm_seq = 0, seq_counter = 0;  // (the armed kernel serves arm_seq, arm_seq + 1, ...)
+  int arm_stream = 1;                      // qstream index of the armed kernel
+  uint32_t armed_first = 0;                // the armed kernel's first number (its `live` report)
+  uint32_t retiring = 0;                   // a rotated-out kernel still waiting for arm_seq's to start
+  uint32_t arm_waves = 0;                  // waves of the armed kernel: kQcSlots (narrow) or kQcCap (wide)
+  std::chrono::steady_clock::time_point last_wide{};  // the last latency-path call of 9..kQcCap signatures
+  std::chrono::steady_clock::time_point armed_at{}, last_qc{};
+  // diagnostics of the last latency-path call (pbftv_qc_stamps)
+  uint64_t qc_ns_entry = 0, qc_ns_handover = 0, qc_ns_total = 0, qc_ns_slots = 0;
+  char hot_end[1] = {};
   // signature state: comb table of G (width gbits) and one table per registered
   // key (width qbits), addressed through qptrs (device array, by key).  Key
   // tables live in blocks (one per registration / add_keys call; slots beyond
@@ -208,34 +229,18 @@ struct Device {
   std::vector<void*> qtab;  // table of key j (registered keys first, then spare slots)
   int gbits = 0, qbits = 0;
   uint32_t nkeys = 0;
-  bool have_keys = false;
   // ecdsa scratch
   DevBuf hashes, sigs, key_idx, bitmap;
   VerifyScratch vs;  // the lane path's stage-1 records, prefix products, key order, result bytes
-  HostBuf stage;  // zero-copy inputs/outputs of the small-batch path (a QcMail mailbox)
-  // the armed latency kernel (k_ecdsa_wave_armed): a persistent server that
-  // waits for the next request's doorbell in `stage`; arm_seq = the request
-  // number it waits for (0: none armed)
+  // the armed kernels' streams, relay words and keeper thread
   hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: a rotation's successor spins beside its predecessor
-  uint32_t arm_seq = 0, seq_counter = 0;  // (the armed kernel serves arm_seq, arm_seq + 1, ...)
-  int arm_stream = 1;                      // qstream index of the armed kernel
-  uint32_t armed_first = 0;                // the armed kernel's first number (its `live` report)
-  uint32_t retiring = 0;                   // a rotated-out kernel still waiting for arm_seq's to start
-  uint32_t arm_waves = 0;                  // waves of the armed kernel: kQcSlots (narrow) or kQcCap (wide)
   DevBuf qrelay;                           // the wide kernels' relay words, one 64-B line per qstream:
                                            // uncached device memory (read and written past the 8 XCDs' L2s, so
                                            // no cache maintenance: an agent-scope acquire per poll would
                                            // invalidate the poller's whole L2)
-  std::chrono::steady_clock::time_point last_wide{};  // the last latency-path call of 9..kQcCap signatures
-  bool mail_registered = false;  // the mailbox is in the arm registry
-  std::chrono::steady_clock::time_point armed_at{}, last_qc{};
   std::thread keeper;  // qc_keeper_loop
   std::condition_variable keeper_cv;
-  bool keeper_stop = false, keeper_idle = false;
   uint64_t rotations = 0;
-  // diagnostics of the last latency-path call (pbftv_qc_stamps)
-  uint64_t qc_ns_entry = 0, qc_ns_handover = 0, qc_ns_total = 0, qc_ns_slots = 0;
-  bool qc_armed_served = false;
   // host-buffer pipeline (pbftv_ecdsa_p256_verify_batch above the latency
   // path): two slots of pinned staging + device inputs, a copy stream
   static constexpr int kSlots = 16;  // chunks staged ahead at most (PBFTV_HOST_SLOTS, default 16)
@@ -576,6 +581,7 @@ struct pbftv_ctx {
   // pbftv_set_latency_path_max): read once, not per call (a cold getenv cost
   // a certificate ~3 us after an idle second)
   std::atomic<uint64_t> wave_max{2048};
+  Device* dev0 = nullptr;  // devs[0], one hop less for the latency path's first (cold) loads
 };
 
 namespace {
@@ -822,6 +828,7 @@ int pbftv_open(pbftv_ctx** out, uint32_t device_mask) {
     }
   }
   if (ctx->devs.empty()) return fail(PBFTV_ENODEV, "no gfx950 device in device_mask");
+  ctx->dev0 = ctx->devs[0].get();
   ctx->wave_max = pbftv::wave_path_max();
   *out = ctx.release();
   return PBFTV_OK;
@@ -1579,19 +1586,24 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
   const auto h_entry = std::chrono::steady_clock::now();
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
   if (n && (!hashes || !sig_rs || !key_idx || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
-  if (n && n <= QcMail::kQcSlots && !ctx->devs.empty()) {
+  if (n && n <= QcMail::kQcSlots && ctx->dev0) {
     // A certificate after an idle second finds this core's caches cold (the
     // caller slept; its core's private caches were flushed): start the misses
     // of the lines the armed path touches now, in parallel, instead of one
     // after another (device lock and state, the mailbox header, slot lines and
-    // result bytes).  A stale mailbox pointer is harmless: a prefetch never faults.
-    const Device* d0 = ctx->devs[0].get();
-    __builtin_prefetch(&d0->mu, 1, 3);
-    __builtin_prefetch(&d0->arm_seq, 1, 3);
+    // verdict bytes: the mailbox's first page).  A stale mailbox pointer is
+    // harmless: a prefetch never faults.
+    const Device* d0 = ctx->dev0;
+    for (const char* q = reinterpret_cast<const char*>(&d0->mu); q <= d0->hot_end; q += 64) __builtin_prefetch(q, 1, 3);
+    __builtin_prefetch(d0->hot_end, 1, 3);
     if (const uint8_t* mb = static_cast<const uint8_t*>(d0->stage.p)) {
       for (size_t off = 0; off < QcMail::arrays_off(); off += 64) __builtin_prefetch(mb + off, 1, 3);
-      __builtin_prefetch(mb + QcMail::res_off(QcMail::kQcCap), 1, 3);
     }
+    // and the caller's buffers
+    for (uint64_t off = 0; off < 32 * n; off += 64) __builtin_prefetch(hashes + off, 0, 3);
+    for (uint64_t off = 0; off < 64 * n; off += 64) __builtin_prefetch(sig_rs + off, 0, 3);
+    __builtin_prefetch(key_idx, 0, 3);
+    __builtin_prefetch(out_bitmap, 1, 3);
   }
   for (auto& dp : ctx->devs)
     if (!dp->have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
@@ -1606,7 +1618,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     // rings, and nothing else -- no launch, no HIP call -- is on its path.
     // Otherwise, or when the armed kernel has run out, one launch of
     // k_ecdsa_wave (up to 2048 signatures, one wave each).
-    Device& d = *ctx->devs[0];
+    Device& d = *ctx->dev0;
     std::lock_guard<std::mutex> lk(d.mu);
     const auto h_in = std::chrono::steady_clock::now();
     d.last_qc = h_in;
@@ -1630,7 +1642,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     m->cap = cap;
     m->n = (uint32_t)n;
     auto launch_plain = [&]() -> int {
-      uint8_t* const hp = st8 + QcMail::hashes_off();
+      uint8_t* const hp = st8 + QcMail::hashes_off(cap);
       uint8_t* const sp = st8 + QcMail::sigs_off(cap);
       uint32_t* const kp = reinterpret_cast<uint32_t*>(st8 + QcMail::keys_off(cap));
       std::memcpy(hp, hashes, 32 * n);
@@ -1654,7 +1666,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     if (d.arm_seq && n <= d.arm_waves) {
       cur = d.arm_seq;
       if (n > QcMail::kQcSlots) {  // the helpers' inputs (slots kQcSlots..n-1), before any slot tag
-        std::memcpy(st8 + QcMail::hashes_off() + 32 * QcMail::kQcSlots, hashes + 32 * QcMail::kQcSlots,
+        std::memcpy(st8 + QcMail::hashes_off(cap) + 32 * QcMail::kQcSlots, hashes + 32 * QcMail::kQcSlots,
                     32 * (n - QcMail::kQcSlots));
         std::memcpy(st8 + QcMail::sigs_off(cap) + 64 * QcMail::kQcSlots, sig_rs + 64 * QcMail::kQcSlots,
                     64 * (n - QcMail::kQcSlots));

@@ -1250,7 +1250,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
       __builtin_amdgcn_s_setprio(3);
       constexpr uint32_t cap = QcMail::kQcCap;  // the armed path's layout (the host relays it out only after a disarm)
       // lanes 0-7 the hash, 8-23 r || s, 24 the key index: one round trip
-      const uint32_t* src = lane < 8    ? reinterpret_cast<const uint32_t*>(base + QcMail::hashes_off() + 32 * b) + lane
+      const uint32_t* src = lane < 8    ? reinterpret_cast<const uint32_t*>(base + QcMail::hashes_off(cap) + 32 * b) + lane
                             : lane < 24 ? reinterpret_cast<const uint32_t*>(base + QcMail::sigs_off(cap) + 64 * b) + (lane - 8)
                                         : reinterpret_cast<const uint32_t*>(base + QcMail::keys_off(cap) + 4 * b);
       const uint32_t v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
