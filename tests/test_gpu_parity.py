@@ -588,3 +588,60 @@ def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypa
         for i in range(24, n_all - 3, 3):
             for v in (a, b):
                 assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all(), i
+
+
+def test_armed_kernels_of_two_contexts_concurrent(oracle_lib):
+    """Two contexts on one GPU, each with its own armed server and keeper,
+    called from two threads at once with certificates of 1-129 signatures
+    (narrow, wide and launched), while a third thread runs lane-path batches
+    on the first context: every bitmap against the oracle, and both contexts
+    served most certificates armed (pbftv_qc_stamps)."""
+    import threading
+    from simple_pbft_amd import Verifier
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=6, per_key=100, seed=91)
+    sigs[::9, 50] ^= 0x04
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    errors, armed = [], {}
+    with Verifier(device_mask=1) as a, Verifier(device_mask=1) as b:
+        a.register_keys(keys)
+        b.register_keys(keys)
+
+        def certs(name, v, seed):
+            rng = np.random.default_rng(seed)
+            got_armed = 0
+            try:
+                for it in range(150):
+                    n = int(rng.choice([1, 3, 3, 4, 8, 67, 100, 129]))
+                    o = rng.choice(n_all, n, replace=False)
+                    got = v.verify_batch(hashes[o], sigs[o], kidx[o])
+                    if not (got == want[o]).all():
+                        errors.append((name, it, n))
+                    got_armed += v.qc_stamps(0)["armed"]
+            except Exception as e:  # noqa: BLE001 -- reported by the main thread
+                errors.append((name, repr(e)))
+            armed[name] = got_armed
+
+        def lanes():
+            rng = np.random.default_rng(7)
+            try:
+                for it in range(6):
+                    o = rng.choice(n_all, 4096, replace=True)
+                    with_path = a.verify_batch(hashes[o], sigs[o], kidx[o])
+                    if not (with_path == want[o]).all():
+                        errors.append(("lanes", it))
+            except Exception as e:  # noqa: BLE001
+                errors.append(("lanes", repr(e)))
+
+        ts = [threading.Thread(target=certs, args=("a", a, 1)), threading.Thread(target=certs, args=("b", b, 2)),
+              threading.Thread(target=lanes)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert not any(t.is_alive() for t in ts), "a caller thread hung"
+    assert not errors, errors[:5]
+    assert armed["a"] >= 60 and armed["b"] >= 60, armed
