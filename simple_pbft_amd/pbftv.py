@@ -579,10 +579,12 @@ class Verifier:
         armed = bool(int(o[2]) & 1)
         r = {"handover_us": float(o[0]) * 1e-3, "total_us": float(o[1]) * 1e-3, "armed": armed,
              "entry_us": float(int(o[2]) >> 32) * 1e-3, "slots_in_us": float((int(o[2]) >> 1) & 0x7FFFFFFF) * 1e-3}
-        if armed and o[5] > o[3]:
-            wall_s = float(o[5] - o[3]) / (float(o[7]) * 1e3)
+        w0, c0, w1, c1, khz = (int(x) for x in (o[3], o[4], o[5], o[6], o[7]))
+        if armed and w1 > w0 and khz:  # (stamps are written only with PBFTV_QC_STAMPS=1)
+            wall_s = (w1 - w0) / (khz * 1e3)
             r["gpu_serve_us"] = wall_s * 1e6
-            r["sclk_mhz"] = float(o[6] - o[4]) / wall_s * 1e-6
+            if c1 > c0:
+                r["sclk_mhz"] = (c1 - c0) / wall_s * 1e-6
         return r
 
     # ---- sha256 / digests
