@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(256, 2) k_sha256_ring(const uint8_t* __restric
   const uint32_t* L0 = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)127);
   const uint32_t lob = (uint32_t)(a & 127u), sh = (uint32_t)(a & 3u);
   const uint32_t D0 = lob >> 2;                  // the message's first dword in line 0
-  const uint32_t nlines = (lob + len + 127u) >> 7;  // lines holding message bytes (>= 1 for len >= 1)
+  const uint32_t nlines = (uint32_t)(((uint64_t)lob + len + 127u) >> 7);  // lines holding message bytes (>= 1 for len >= 1)
   uint32_t L[32];
   // lines 0 and 1 (blocks 0 and 1 need nothing past line 1).  An empty message
   // on a line boundary has no line (it may sit at the very end of a mapping):
