@@ -329,10 +329,12 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
  * table): pbftv_add_keys appends k keys as indices nkeys .. nkeys + k - 1 at the
  * registered geometry (PBFTV_ENOMEM if their tables do not fit);
  * pbftv_set_key replaces key `index` (< nkeys) in place.  Both need a prior
- * pbftv_register_keys.  They, and pbftv_register_keys, first wait for ALL work
- * queued on the GPU (hipDeviceSynchronize: verifies enqueued on caller
- * streams by the *_dev entry points included), so no verify in flight reads a
- * table, validity flag or table pointer while it is rewritten.  If any device
+ * pbftv_register_keys.  They, and pbftv_register_keys, first wait for every
+ * verify of THIS context still in flight -- on the library's streams, on
+ * streams from pbftv_stream_create and on any other caller stream a *_dev
+ * call was given -- so no verify reads a table, validity flag or table
+ * pointer while it is rewritten.  Other contexts on the GPU are not waited
+ * for (they read their own key tables).  If any device
  * fails, every device of the context drops its key set (PBFTV_ENOKEYS until
  * the next successful pbftv_register_keys), so shards never disagree on the
  * keys. */

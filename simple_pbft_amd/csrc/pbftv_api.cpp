@@ -267,6 +267,11 @@ struct Device {
   // verifies on two such streams run concurrently (batch j + 1's scalar stage
   // in the wave slots batch j's comb leaves free) instead of queueing on d.vs
   std::map<hipStream_t, std::unique_ptr<VerifyScratch>> stream_scratch;
+  // caller streams the library did not create that a wave-path verify (no
+  // device scratch, so no scratch_ev fence) was enqueued on since the last key
+  // change: an event recorded after each such enqueue (events stay valid when
+  // the caller destroys its stream); ctx_quiesce waits for them all
+  std::map<hipStream_t, hipEvent_t> reader_ev;
   // kernel timing (events recorded around launches while ctx timing is on)
   const bool* timing = nullptr;
   const std::atomic<uint64_t>* wave_max = nullptr;  // the context's latency-path threshold
@@ -437,6 +442,44 @@ hipError_t qc_disarm(Device& d) {
   for (hipStream_t q : d.qstream)
     if (q) HIP_TRY_E(hipStreamSynchronize(q));
   return hipSuccess;
+}
+
+// Before a key change rewrites this context's key tables, key_valid or qptrs
+// in place: nothing of THIS context may still read them.  Its armed kernels
+// leave (qc_disarm), then its own streams drain, and every caller stream it
+// was given: streams from pbftv_stream_create are known (stream_scratch); any
+// other caller stream shares the device scratch, whose last use is fenced by
+// scratch_ev, and every use waited for the one before it (scratch_acquire).
+// Other contexts on the GPU are not waited for: their kernels read their own
+// key tables, and a G table is never rewritten in place (a new width is a new
+// table).  Frees inside the key change still quiesce the GPU (DevBuf).
+hipError_t ctx_quiesce(Device& d) {
+  HIP_TRY_E(qc_disarm(d));
+  for (hipStream_t s : {d.stream, d.stream2, d.cstream})
+    if (s) HIP_TRY_E(hipStreamSynchronize(s));
+  for (auto& kv : d.stream_scratch) HIP_TRY_E(hipStreamSynchronize(kv.first));
+  if (d.scratch_st && d.scratch_st != d.stream && d.scratch_ev) HIP_TRY_E(hipEventSynchronize(d.scratch_ev));
+  for (auto& kv : d.reader_ev) HIP_TRY_E(hipEventSynchronize(kv.second));
+  for (auto& kv : d.reader_ev) (void)hipEventDestroy(kv.second);
+  d.reader_ev.clear();
+  return hipSuccess;
+}
+
+// a verify that reads the key tables was just enqueued on st without the
+// device scratch: fence it for the next key change if st is a caller stream
+// the context does not know
+hipError_t fence_reader(Device& d, hipStream_t st) {
+  if (st == d.stream || st == d.stream2 || d.stream_scratch.count(st)) return hipSuccess;
+  if (d.reader_ev.size() >= 64 && !d.reader_ev.count(st)) {
+    // a caller cycling through many streams: settle the fenced ones instead of
+    // keeping an event per stream handle forever
+    for (auto& kv : d.reader_ev) HIP_TRY_E(hipEventSynchronize(kv.second));
+    for (auto& kv : d.reader_ev) (void)hipEventDestroy(kv.second);
+    d.reader_ev.clear();
+  }
+  hipEvent_t& ev = d.reader_ev[st];
+  if (!ev) HIP_TRY_E(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  return hipEventRecord(ev, st);
 }
 
 void qc_keeper_loop(Device* d);
@@ -856,6 +899,8 @@ void pbftv_close(pbftv_ctx* ctx) {
       b->release();  // explicit, with this device current (the destructors are a backstop)
     for (HostBuf* b : {&d->stage, &d->mstage, &d->mout}) b->release();
     if (d->scratch_ev) (void)hipEventDestroy(d->scratch_ev);
+    for (auto& kv : d->reader_ev) (void)hipEventDestroy(kv.second);
+    d->reader_ev.clear();
     if (d->stream2) {
       (void)hipStreamSynchronize(d->stream2);
       (void)hipStreamDestroy(d->stream2);
@@ -1326,15 +1371,11 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
     auto t0 = std::chrono::steady_clock::now();
-    // every armed latency kernel on this GPU leaves first (this context's reads
-    // the tables; any context's would hold the device synchronisation below)
-    GpuQuiesce quiet(d.id);
-    HIP_TRY(qc_disarm(d));
+    // nothing of this context still reads the tables, key_valid or qptrs this
+    // call rewrites in place: its armed kernels, its streams and the caller
+    // streams it was given (a verify enqueued on one with *_dev)
+    HIP_TRY(ctx_quiesce(d));
     d.have_keys = false;
-    // every stream of the GPU, not only ours: a verify enqueued on a caller
-    // stream (pbftv_stream_create + *_dev) may still read the tables, key_valid
-    // or qptrs this call rewrites in place
-    HIP_TRY(hipDeviceSynchronize());
     // another process or context can take HBM between the free-memory query
     // and the allocations: on ENOMEM this device's tables are freed and the
     // geometry is chosen again from what is free then (3 attempts)
@@ -1369,9 +1410,7 @@ int pbftv_add_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8_t* o
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    GpuQuiesce quiet(d.id);  // (as in pbftv_register_keys)
-    HIP_TRY(qc_disarm(d));
-    HIP_TRY(hipDeviceSynchronize());  // caller streams too: qptrs and key_valid are rewritten
+    HIP_TRY(ctx_quiesce(d));  // (as in pbftv_register_keys: qptrs and key_valid are rewritten)
     return build_key_tables(d, le, d.nkeys, k, first ? valid.data() : nullptr);
   });
   if (rc != PBFTV_OK) {
@@ -1398,9 +1437,7 @@ int pbftv_set_key(pbftv_ctx* ctx, uint32_t index, const uint8_t* pub_xy, uint8_t
   int rc = for_each_device(ctx, [&](Device& d, bool first) -> int {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_TRY(hipSetDevice(d.id));
-    GpuQuiesce quiet(d.id);  // (as in pbftv_register_keys)
-    HIP_TRY(qc_disarm(d));
-    HIP_TRY(hipDeviceSynchronize());  // no verify on any stream (caller streams too) still reads the old table
+    HIP_TRY(ctx_quiesce(d));  // no verify of this context (caller streams too) still reads the old table
     return build_key_tables(d, le, index, 1, first ? &valid : nullptr);
   });
   if (rc != PBFTV_OK) {
@@ -1436,6 +1473,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
       return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, d_hashes, d_sigs, d_key_idx, n, d.key_valid.as<uint32_t>(),
                                       d.nkeys, d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), d_bitmap, nullptr, st);
     }));
+    HIP_TRY(fence_reader(d, st));
     return PBFTV_OK;
   }
   if (!own) {

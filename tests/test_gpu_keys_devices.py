@@ -129,12 +129,30 @@ def test_two_device_registration_geometry(two_devices, oracle_lib):
     assert v.verify_batch(np.concatenate([H, H[:4]]), np.concatenate([S, S[:4]]), K2).all()
 
 
+def ctypes_void(p):
+    import ctypes
+    return ctypes.c_void_p(p)
+
+
+def _foreign_stream():
+    """A HIP stream the library did not create (hipStreamCreateWithFlags,
+    non-blocking), as a caller that owns its streams would pass one."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(st), ctypes.c_uint(1)) == 0
+    return hip, st.value
+
+
+@pytest.mark.parametrize("stream_kind", ["library", "foreign"])
 @pytest.mark.parametrize("path_n", [64, 40_000])  # the wave kernel (<= 2048) and the lane path
-def test_set_key_waits_for_caller_stream_verifies(oracle_lib, path_n, monkeypatch):
+def test_set_key_waits_for_caller_stream_verifies(oracle_lib, path_n, stream_kind, monkeypatch):
     """a verify enqueued on a CALLER stream (pbftv_stream_create +
-    verify_batch_dev) must still see the old key table when pbftv_set_key
-    replaces that key right after the enqueue: set_key waits for every stream
-    of the GPU before it rewrites the table in place."""
+    verify_batch_dev, or a stream the caller made itself) must still see the
+    old key table when pbftv_set_key replaces that key right after the
+    enqueue: set_key waits for every stream this context was given before it
+    rewrites the table in place (round 4: only this context's work, not the
+    whole device)."""
     from simple_pbft_amd import Verifier
     monkeypatch.setenv("PBFTV_GBITS", "24")
     monkeypatch.setenv("PBFTV_QBITS", "16")
@@ -145,7 +163,11 @@ def test_set_key_waits_for_caller_stream_verifies(oracle_lib, path_n, monkeypatc
     with Verifier(device_mask=1) as v:
         assert v.register_keys(keys).all()
         bufs = [v.to_device(0, H), v.to_device(0, S), v.to_device(0, K), v.alloc(0, (path_n + 7) // 8)]
-        side = v.stream_create(0)
+        hip = None
+        if stream_kind == "library":
+            side = v.stream_create(0)
+        else:
+            hip, side = _foreign_stream()
         try:
             for _ in range(3):
                 bufs[3].zero()
@@ -160,7 +182,11 @@ def test_set_key_waits_for_caller_stream_verifies(oracle_lib, path_n, monkeypatc
             got = v.verify_batch(H, S, K)
             assert got.tolist() == (K != 0).tolist()
         finally:
-            v.stream_destroy(0, side)
+            if hip is None:
+                v.stream_destroy(0, side)
+            else:
+                v.stream_wait(0, side)
+                hip.hipStreamDestroy(ctypes_void(side))
             for b in bufs:
                 b.free()
 
