@@ -168,14 +168,21 @@ def test_set_key_waits_for_caller_stream_verifies(oracle_lib, path_n, stream_kin
             side = v.stream_create(0)
         else:
             hip, side = _foreign_stream()
+        # a queue of verifies several ms long, so the rewrite would overlap it
+        deep = 40 if path_n <= 2048 else 8
+        outs = [v.alloc(0, (path_n + 7) // 8) for _ in range(deep)]
+        bufs += outs
         try:
             for _ in range(3):
-                bufs[3].zero()
-                v.verify_batch_dev(0, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, path_n, bufs[3].ptr, stream=side)
+                for o in outs:
+                    o.zero()
+                for o in outs:
+                    v.verify_batch_dev(0, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, path_n, o.ptr, stream=side)
                 assert v.set_key(0, keys[1])  # key 0 now holds key 1's point
                 v.stream_wait(0, side)
-                got = np.unpackbits(bufs[3].to_host(), bitorder="little")[:path_n].astype(bool)
-                assert got.all(), "a verify queued before set_key saw the new table"
+                for j, o in enumerate(outs):
+                    got = np.unpackbits(o.to_host(), bitorder="little")[:path_n].astype(bool)
+                    assert got.all(), f"verify {j} queued before set_key saw the new table"
                 assert v.set_key(0, keys[0])
             # after the change, key-0 signatures fail under index 0
             v.set_key(0, keys[1])
