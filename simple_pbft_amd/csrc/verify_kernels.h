@@ -1350,7 +1350,21 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
 
 template <int WG, int WQ>
 void launch_armed_w(const ArmArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3((a.relay ? QcMail::kQcCap : QcMail::kQcSlots) / 4), dim3(256), 0,
+  // PBFTV_QC_EXCLUSIVE_CU=1 (opt-in): every armed workgroup takes its CU's
+  // whole LDS, so no other kernel's block shares a CU -- and a SIMD's issue
+  // slots -- with the armed waves (a certificate under a concurrent batch);
+  // the batch then runs on the other CUs.  Read at every arming.
+  const char* e = getenv("PBFTV_QC_EXCLUSIVE_CU");
+  const uint32_t lds = e && e[0] == '1' ? 160u * 1024u : 0u;
+  if (lds) {
+    static bool attr = false;  // (per instantiation)
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ecdsa_wave_armed<WG, WQ>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+  }
+  hipLaunchKernelGGL((k_ecdsa_wave_armed<WG, WQ>), dim3((a.relay ? QcMail::kQcCap : QcMail::kQcSlots) / 4), dim3(256), lds,
                      st, a);
 }
 
