@@ -645,3 +645,32 @@ def test_armed_kernels_of_two_contexts_concurrent(oracle_lib):
         assert not any(t.is_alive() for t in ts), "a caller thread hung"
     assert not errors, errors[:5]
     assert armed["a"] >= 60 and armed["b"] >= 60, armed
+
+
+def test_armed_exclusive_cu_option(oracle_lib, monkeypatch):
+    """PBFTV_QC_EXCLUSIVE_CU=1: the armed workgroups take their CUs' whole LDS
+    (no batch block shares their SIMDs).  Certificates narrow and wide are
+    still served armed and right, also while a lane-path batch runs."""
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_EXCLUSIVE_CU", "1")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=5, per_key=80, seed=95)
+    sigs[::6, 37] ^= 0x10
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    rng = np.random.default_rng(96)
+    armed = 0
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        for it, n in enumerate([3, 3, 4, 67, 67, 100, 3, 8, 1] * 4):
+            o = rng.choice(n_all, n, replace=False)
+            assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all(), (it, n)
+            armed += v.qc_stamps(0)["armed"]
+        o = rng.choice(n_all, 5000)
+        assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all()  # a batch beside the armed CUs
+        for it in range(10):
+            o = rng.choice(n_all, 3, replace=False)
+            assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all(), it
+    assert armed >= 24, armed
