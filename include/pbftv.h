@@ -96,10 +96,29 @@ int pbftv_stream_destroy(pbftv_ctx* ctx, int dev, void* stream);
 int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
 
 /* Batches of up to n signatures take the latency path (one wave per
- * signature; the armed kernel for <= 8); larger ones the lane path (scalar +
- * comb kernels).  Default 2048, or PBFTV_WAVE_MAX at pbftv_open; 0 disables
- * the latency path.  Read once per call from the context, never from the
- * environment on the call path. */
+ * signature); larger ones the lane path (scalar + comb kernels).  Default
+ * 2048, or PBFTV_WAVE_MAX at pbftv_open; 0 disables the latency path.  Read
+ * once per call from the context, never from the environment on the call
+ * path.
+ *
+ * Up to 128 signatures of a latency-path call are served by a resident
+ * "armed" kernel polling a doorbell in pinned host memory (8 slot waves; 120
+ * helper waves more once calls of 9..128 signatures have been seen), so no
+ * launch is on the call's path.  A keeper thread per device replaces it
+ * before its budget runs out for as long as calls keep coming.  Environment,
+ * read at every arming:
+ *   PBFTV_QC_ARM=0            never arm (every call launches);
+ *   PBFTV_QC_ARM_MS=100       one armed kernel's budget (ms);
+ *   PBFTV_QC_KEEP_MS=10000    keep one armed this long after the last call
+ *                             (0: no keeper; the kernel runs out);
+ *   PBFTV_QC_WIDE=0           never arm the 128-wave form;
+ *   PBFTV_QC_EXCLUSIVE_CU=1   armed workgroups take whole CUs (faster
+ *                             certificates beside a concurrent batch, at a
+ *                             few % of that batch's rate);
+ *   PBFTV_QC_STAMPS=1         the kernel records GPU timestamps
+ *                             (pbftv_qc_stamps*).
+ * pbftv_dev_free / pbftv_host_free and the library's own frees stop every
+ * armed kernel on the GPU first (hipFree waits for every kernel). */
 int pbftv_set_latency_path_max(pbftv_ctx* ctx, uint64_t n);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every
