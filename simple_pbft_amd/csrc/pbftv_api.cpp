@@ -1627,7 +1627,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
   const auto h_entry = std::chrono::steady_clock::now();
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
   if (n && (!hashes || !sig_rs || !key_idx || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
-  if (n && n <= QcMail::kQcSlots && ctx->dev0) {
+  if (n && n <= QcMail::kQcCap && ctx->dev0) {
     // A certificate after an idle second finds this core's caches cold (the
     // caller slept; its core's private caches were flushed): start the misses
     // of the lines the armed path touches now, in parallel, instead of one
@@ -1639,11 +1639,20 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     __builtin_prefetch(d0->hot_end, 1, 3);
     if (const uint8_t* mb = static_cast<const uint8_t*>(d0->stage.p)) {
       for (size_t off = 0; off < QcMail::arrays_off(); off += 64) __builtin_prefetch(mb + off, 1, 3);
+      if (n > QcMail::kQcSlots) {  // the helpers' input arrays this call writes
+        const uint64_t h = n - QcMail::kQcSlots;
+        for (uint64_t off = 0; off < 32 * h; off += 64)
+          __builtin_prefetch(mb + QcMail::hashes_off() + 32 * QcMail::kQcSlots + off, 1, 3);
+        for (uint64_t off = 0; off < 64 * h; off += 64)
+          __builtin_prefetch(mb + QcMail::sigs_off(QcMail::kQcCap) + 64 * QcMail::kQcSlots + off, 1, 3);
+        for (uint64_t off = 0; off < 4 * h; off += 64)
+          __builtin_prefetch(mb + QcMail::keys_off(QcMail::kQcCap) + 4 * QcMail::kQcSlots + off, 1, 3);
+      }
     }
     // and the caller's buffers
     for (uint64_t off = 0; off < 32 * n; off += 64) __builtin_prefetch(hashes + off, 0, 3);
     for (uint64_t off = 0; off < 64 * n; off += 64) __builtin_prefetch(sig_rs + off, 0, 3);
-    __builtin_prefetch(key_idx, 0, 3);
+    for (uint64_t off = 0; off < 4 * n; off += 64) __builtin_prefetch(key_idx + off / 4, 0, 3);
     __builtin_prefetch(out_bitmap, 1, 3);
   }
   for (auto& dp : ctx->devs)
