@@ -316,6 +316,31 @@ func (x *Ctx) QCVerify(hashes [][32]byte, sigs [][64]byte, keyIdx []uint32, quor
 	return bits(bm, n), int(acc), q != 0, nil
 }
 
+// SetLatencyPathMax: batches of up to n signatures take the latency path (one
+// wave per signature; up to 128 of them served by the resident armed kernel
+// with no launch on the call's path); larger ones the throughput path.  The
+// default is 2048; 0 sends every batch to the throughput path.
+func (x *Ctx) SetLatencyPathMax(n uint64) error {
+	return call(func() C.int { return C.pbftv_set_latency_path_max(x.c, C.uint64_t(n)) })
+}
+
+// QCStamps says where the last latency-path call's time went
+// (pbftv_qc_stamps): host ns from entry to hand-over (doorbell rung or kernel
+// launched) and to return, and whether the armed kernel served it.
+type QCStamps struct {
+	HandoverNs, TotalNs uint64
+	Armed               bool
+}
+
+func (x *Ctx) QCStamps() (QCStamps, error) {
+	var out [8]C.uint64_t
+	err := call(func() C.int { return C.pbftv_qc_stamps(x.c, 0, &out[0]) })
+	if err != nil {
+		return QCStamps{}, err
+	}
+	return QCStamps{HandoverNs: uint64(out[0]), TotalNs: uint64(out[1]), Armed: uint64(out[2])&1 == 1}, nil
+}
+
 // DERToRS is the parse half of crypto/ecdsa.VerifyASN1 (go1.19 cryptobyte
 // strictness).  A rejected encoding returns ok = false and r = s = 0, which
 // VerifySigs turns into a false, so VerifyASN1(pub, h, der) ==
