@@ -67,6 +67,34 @@ def test_sha256_empty_batch_and_empty_message(ver):
     assert ver.hash_hex(b"") == hashlib.sha256(b"").hexdigest()
 
 
+def test_sha256_empty_messages_on_line_boundaries(ver):
+    """Empty messages at 128-B-aligned offsets (the ring kernel reads no line
+    for them), one at the very end of the data, among 1..300-B neighbours
+    that end exactly on line boundaries."""
+    rng = np.random.default_rng(19)
+    lens, offs, pos = [], [], 0
+    for i in range(600):
+        if i % 3 == 0:
+            pos = (pos + 127) // 128 * 128  # an empty message on a line boundary
+            lens.append(0)
+        else:
+            lens.append(int(rng.integers(1, 300)))
+            if i % 3 == 2:  # ends exactly on a line boundary
+                lens[-1] = (pos + lens[-1] + 127) // 128 * 128 - pos
+        offs.append(pos)
+        pos += lens[-1]
+    pos = (pos + 127) // 128 * 128
+    lens.append(0)
+    offs.append(pos)  # empty, at the end of the data
+    data = np.frombuffer(rng.bytes(pos), np.uint8).copy()
+    lengths = np.array(lens, np.uint32)
+    offsets = np.array(offs, np.uint64)
+    got = ver.sha256_batch(data, offsets, lengths)
+    for i in range(len(lens)):
+        m = data[offs[i]:offs[i] + lens[i]].tobytes()
+        assert got[i].tobytes() == hashlib.sha256(m).digest(), (i, lens[i], offs[i])
+
+
 def test_digest_check(ver):
     rng = np.random.default_rng(3)
     msgs = [rng.bytes(int(l)) for l in rng.integers(0, 300, 777)]
