@@ -46,6 +46,22 @@ __global__ void __launch_bounds__(256, WAVES) kbench(const uint4* __restrict__ t
       xyzz_madd_s(acc, ex, ey);
     }
     for (int l = 0; l < 9; ++l) out[lane * 9 + l] = acc.x.v[l] ^ acc.zz.v[l] ^ acc.y.v[l] ^ acc.zzz.v[l];
+  } else if constexpr (V == 3) {
+    // the comb's own step (comb_step_s's body): the y negation folded into
+    // the entry unpacking, the W = sigma Y accumulator
+    xyzz_s acc;
+    acc.x = x; acc.y = y; fe_set(acc.zz, kOneP); fe_set(acc.zzz, kOneP);
+    bool neg = false;
+    for (int i = 0; i < iters; ++i) {
+      const uint4* p = tab + ((lane + 7 * i + 1) & 63) * 4;
+      uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];
+      uint32_t w[16] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w, e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w};
+      fe ex, ey;
+      entry_to_fe_cneg(ex, ey, w, ((lane + i) & 1) != neg);
+      xyzz_madd_s_flip(acc, ex, ey);
+      neg = !neg;
+    }
+    for (int l = 0; l < 9; ++l) out[lane * 9 + l] = acc.x.v[l] ^ acc.zz.v[l] ^ acc.y.v[l] ^ acc.zzz.v[l];
   } else {
     xyzz acc;
     acc.x = x; acc.y = y; fe_set(acc.zz, kOneP); fe_set(acc.zzz, kOneP);
@@ -103,5 +119,7 @@ int main() {
   run<2, 2>("madd-2008-s xyzz signed", tab, out, blocks, iters);
   run<2, 3>("madd-2008-s xyzz signed", tab, out, blocks, iters);
   run<2, 4>("madd-2008-s xyzz signed", tab, out, blocks, iters);
+  run<3, 2>("comb step (flip, cneg)", tab, out, blocks, iters);
+  run<3, 4>("comb step (flip, cneg)", tab, out, blocks, iters);
   return 0;
 }
