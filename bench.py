@@ -141,6 +141,170 @@ def dist_env():
     return ws, rank, local
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list, data_dir: str | None) -> int:
+    """`bench.py --gpus N` started as ONE process (the driver's plain form):
+    start N rank processes of this script, one per GPU, exactly as
+    torch.distributed.run would (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*),
+    and exit with the first failing rank's code.  This process never touches
+    a GPU (it only generated the batch, shared read-only via data_dir), so
+    starting children from it is safe.  Rank 0's stdout is ours: the JSON line."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PBFTV_BENCH_SPAWNED="1")
+        if data_dir:
+            env["PBFTV_BENCH_DATA"] = data_dir
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr, start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the others\n")
+                    for q in live:
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    return rc
+
+
+def save_batch(n_global: int, keys: int) -> str:
+    """config 4 generated once by the launching process and shared with the
+    ranks through read-only files (tmpfs when there is one): N ranks would
+    otherwise each sign the same million messages on the same host cores."""
+    import tempfile
+    base = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+    dd = tempfile.mkdtemp(prefix="pbftv_bench_", dir=base)
+    pub, H, S, K, ok = synth.config4(n_global, n_keys=keys, seed=0x50424654)
+    for name, a in (("pub", pub), ("H", H), ("S", S), ("K", K), ("ok", ok)):
+        np.save(os.path.join(dd, name + ".npy"), a)
+    return dd
+
+
+def load_batch(dd: str):
+    return tuple(np.load(os.path.join(dd, name + ".npy"), mmap_mode="r") for name in ("pub", "H", "S", "K", "ok"))
+
+
+def in_context_leg(ws: int, share: bool, pub, H, S, K, ok, steps: int, warmup_ms: float, reps: int = 5) -> dict:
+    """The product's own multi-device path, in ONE process: one context over the
+    N GPUs, what the Go drop-in gets from pbftv_open(&ctx, 0).
+      host_path:     the global batch from host memory through
+                     pbftv_ecdsa_p256_verify_batch, which splits it into
+                     contiguous 512-aligned shards, one host thread + stream
+                     per device, and concatenates the bitmaps (run_sharded,
+                     pbftv_api.cpp plan_shards);
+      device_resident: the same shards resident in each device's HBM, one
+                     caller thread per device issuing pbftv_ecdsa_p256_verify_batch_dev
+                     on two library streams (as the per-rank processes do).
+    share: every logical device on GPU 0 (PBFTV_ALIAS_DEVICES; a flow rehearsal
+    on a one-GPU box, not a scaling number)."""
+    import threading
+    from simple_pbft_amd.sharding import plan_shards
+    saved = os.environ.get("PBFTV_ALIAS_DEVICES")
+    if share:
+        os.environ["PBFTV_ALIAS_DEVICES"] = str(ws)
+    ver = Verifier(device_mask=1 if share else (1 << ws) - 1)
+    out = {"what": "one process, one pbftv context over the N devices (pbftv_open device_mask = all)",
+           "shared_device_rehearsal": share}
+    bufs = []
+    try:
+        ndev = ver.device_count()
+        if ndev != ws:
+            raise RuntimeError(f"in_context: the context sees {ndev} devices, --gpus asked for {ws}")
+        out["devices"] = [ver.device_id(i) for i in range(ndev)]
+        H, S, K = (np.ascontiguousarray(a) for a in (H, S, K))
+        ok = np.asarray(ok, bool)
+        n = len(K)
+        t = time.perf_counter()
+        valid = ver.register_keys(np.ascontiguousarray(pub))
+        out["registration_wall_s"] = time.perf_counter() - t
+        assert valid.all()
+        gb, qb, tb = ver.table_config()
+        out["comb_window_bits"] = {"G": gb, "keys": qb}
+        ver.verify_batch(H[:65536], S[:65536], K[:65536])  # first-touch of the host pipeline
+        best, got = 1e9, None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            got = ver.verify_batch(H, S, K)
+            best = min(best, time.perf_counter() - t0)
+        out["host_path"] = {"verifies_per_s": n / best, "ms": best * 1e3, "check": bool((got == ok).all()),
+                            "reps": reps, "what": "pageable host buffers, the best of reps"}
+        shards = plan_shards(n, ndev)
+        per = []
+        for dv, (lo, hi) in enumerate(shards):
+            dh, ds, dk = (ver.to_device(dv, a[lo:hi]) for a in (H, S, K))
+            sts = [ver.stream_create(dv) for _ in range(2)]
+            dbs = [ver.alloc(dv, (hi - lo + 7) // 8 + 1) for _ in sts]
+            bufs += [dh, ds, dk] + dbs
+            per.append((dv, lo, hi, dh, ds, dk, sts, dbs))
+
+        def run(item, k):
+            dv, lo, hi, dh, ds, dk, sts, dbs = item
+            for j in range(k):
+                ver.verify_batch_dev(dv, dh.ptr, ds.ptr, dk.ptr, hi - lo, dbs[j & 1].ptr, stream=sts[j & 1])
+            for st in sts:
+                ver.stream_wait(dv, st)
+
+        def all_devices(k):
+            th = [threading.Thread(target=run, args=(it, k)) for it in per]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < warmup_ms * 1e-3:
+            all_devices(8)
+        t0 = time.perf_counter()
+        all_devices(steps)
+        el = time.perf_counter() - t0
+        chk = True
+        for dv, lo, hi, dh, ds, dk, sts, dbs in per:
+            for db in dbs:
+                chk &= bool((np.unpackbits(db.to_host(), bitorder="little")[:hi - lo].astype(bool) == ok[lo:hi]).all())
+        out["device_resident"] = {"verifies_per_s": n * steps / el, "ms_per_step": el / steps * 1e3,
+                                  "steps": steps, "check": chk, "shards": [[lo, hi] for _, lo, hi, *_ in per]}
+    finally:
+        for b in bufs:
+            b.free()
+        ver.close()
+        if share:
+            if saved is None:
+                os.environ.pop("PBFTV_ALIAS_DEVICES", None)
+            else:
+                os.environ["PBFTV_ALIAS_DEVICES"] = saved
+    return out
+
+
 class Dist:
     def __init__(self, ws):
         self.ws = ws
@@ -750,6 +914,8 @@ def main():
                          "owns its verify scratch), so batch j+1's scalar stage overlaps batch j's comb; 0 = the "
                          "context's own stream")
     ap.add_argument("--no-extras", action="store_true", help="skip QC latency, host path, CPU baselines, other configs")
+    ap.add_argument("--no-in-context", action="store_true",
+                    help="N > 1: skip the one-process leg over one N-device context (in_context)")
     ap.add_argument("--sha-only", action="store_true", help="only configs[4] (SHA-256 digest kernel), one JSON line")
     args = ap.parse_args()
     if args.sha_only:
@@ -759,11 +925,37 @@ def main():
         return
 
     ws, rank, local = dist_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the plain `python bench.py --gpus N`: one rank process per GPU, started here
+        dd = None if args.weak else save_batch(args.n, args.keys)
+        try:
+            rc = spawn_ranks(args.gpus, sys.argv[1:], dd)
+        finally:
+            if dd:
+                import shutil
+                shutil.rmtree(dd, ignore_errors=True)
+        sys.exit(rc)
+    if args.gpus != ws:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} rank processes: launch with "
+                         f"--nproc-per-node {args.gpus}, or without torch.distributed.run")
     d = Dist(ws)
+    if os.environ.get("PBFTV_BENCH_PROBE") == "1":
+        # launcher check without a GPU (tests/test_dist.py): the ranks that came up
+        seen = d.sum(1.0)
+        if rank == 0:
+            print(json.dumps({"probe": True, "world_size": ws, "ranks_seen": seen, "gpus": args.gpus,
+                              "spawned": os.environ.get("PBFTV_BENCH_SPAWNED") == "1",
+                              "shared_data": os.environ.get("PBFTV_BENCH_DATA") is not None}), flush=True)
+        d.close()
+        return
     # one GPU per rank; PBFTV_BENCH_SHARE_DEVICE=1 puts every rank on device 0
     # (only to rehearse the N > 1 flow on a 1-GPU box -- not a scaling number)
     share = os.environ.get("PBFTV_BENCH_SHARE_DEVICE") == "1"
     ver = Verifier(device_mask=1 if share else 1 << local)
+    if ver.device_count() != 1 or (not share and ver.device_id(0) != local):
+        raise SystemExit(f"bench.py rank {rank}: expected GPU {local}, the context has "
+                         f"{[ver.device_id(i) for i in range(ver.device_count())]}")
+    glob = None
     if args.weak:
         n_global, lo = args.n * ws, 0
         n = args.n
@@ -775,8 +967,13 @@ def main():
         per = -(-per // 512) * 512
         lo, hi = min(n_global, rank * per), min(n_global, (rank + 1) * per)
         n = hi - lo
-        pub, H, S, K, ok = synth.config4(n_global, n_keys=args.keys, seed=0x50424654)
-        H, S, K, ok = H[lo:hi], S[lo:hi], K[lo:hi], ok[lo:hi]
+        if os.environ.get("PBFTV_BENCH_DATA"):
+            pub, H, S, K, ok = load_batch(os.environ["PBFTV_BENCH_DATA"])
+        else:
+            pub, H, S, K, ok = synth.config4(n_global, n_keys=args.keys, seed=0x50424654)
+        glob = (pub, H, S, K, ok)
+        H, S, K, ok = (np.ascontiguousarray(a[lo:hi]) for a in (H, S, K, ok))
+        pub = np.ascontiguousarray(pub)
     if share:  # ranks sharing one GPU register one after the other: each sizes its tables from what is free
         for r in range(ws):
             if r == rank:
@@ -1001,13 +1198,21 @@ def main():
             out["qc_latency_us"]["in_batch_us_per_cert"] = {
                 "n4_3sigs": oc["config2"]["ms"] * 1e3 / oc["config2"]["certs"],
                 "n100_67sigs": oc["config3"]["ms"] * 1e3 / oc["config3"]["certs"]}
-        print(json.dumps(out), flush=True)
     for b in [dh, ds, dk] + dbs:
         b.free()
     for st in streams:
         if st is not None:
             ver.stream_destroy(0, st)
-    ver.close()
+    ver.close()  # every rank's tables leave HBM before the one-context leg builds its own
+    d.barrier()
+    if rank == 0 and ws > 1 and glob is not None and not args.no_in_context:
+        try:
+            out["in_context"] = in_context_leg(ws, share, *glob, steps=args.steps, warmup_ms=args.warmup_ms)
+        except Exception as e:  # noqa: BLE001 -- reported in the line; the per-rank value above stands
+            out["in_context"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    d.barrier()
     d.close()
 
 

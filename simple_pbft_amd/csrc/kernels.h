@@ -114,24 +114,31 @@ uint64_t wave_path_max();
 // (k_ecdsa_wave_armed) waiting for that number serves it; stop = seq cancels
 // the armed kernel, which then reports expired = seq (verify_kernels.h); so
 // does any change of halt (a disarm, or the process-wide quiesce of a GPU,
-// pbftv_api.cpp).  live = the first request number of the newest armed kernel
-// that has started (written by it: a rotation retires the old one after that).
+// pbftv_api.cpp).  Two armed kernels can be resident at once (a rotation's
+// successor beside its predecessor, one per armed stream), so each armed
+// stream slot has its OWN expired word and its own live words (each wave's
+// first request number once it is resident): two kernels leaving at once
+// (a halt bump) cannot overwrite each other's report.
 // The first kQcSlots signatures are also written to their own 3-line slot
 // (slot_off): line 0 = {tag, n, key, 0, hash[32], 0, 0, 0, tag}, line 1 =
 // {tag, 0, 0, 0, r[32], 0, 0, 0, tag}, line 2 likewise with s; the tags (the
 // request number) are written after their line's data, the last dword first.
 struct QcMail {
-  uint32_t bell, n, stop, expired, cap, halt, live, pad[9];
+  uint32_t bell, n, stop, expired_s0, cap, halt, expired_s1, pad[9];  // (stop at dword 2, halt at 5: read by the kernel)
   static constexpr uint32_t kQcSlots = 8;
   static constexpr uint32_t kQcCap = 128;  // signatures per call up to which the mailbox is laid out at cap = 128
+  static constexpr int kArmSlots = 2;      // armed stream slots (pbftv_api.cpp Device::qstream)
+  // the expired word of armed stream slot s
+  __host__ __device__ uint32_t* expired(int s) { return s ? &expired_s1 : &expired_s0; }
   static constexpr size_t slot_off(uint32_t i) { return 64 + 192 * (size_t)i; }
-  // each armed wave's first request number once it is resident (4 B per wave)
-  static constexpr size_t live_off() { return 64 + 192 * (size_t)kQcSlots; }
+  // each armed wave's first request number once it is resident (4 B per
+  // wave), per armed stream slot
+  static constexpr size_t live_off(int s = 0) { return 64 + 192 * (size_t)kQcSlots + 4 * (size_t)kQcCap * s; }
   // one verdict byte per signature, right after the live words: with the
   // header and the slot lines in the mailbox's FIRST 4-KiB page, so a
   // certificate of <= kQcSlots touches one page of it (one TLB entry on the
   // host, one translation on the GPU, both warm from the polling)
-  static constexpr size_t res_off(uint32_t = kQcCap) { return live_off() + 4 * (size_t)kQcCap; }
+  static constexpr size_t res_off(uint32_t = kQcCap) { return live_off(kArmSlots); }
   // the input arrays of signatures kQcSlots.. (and of every signature on the
   // launched path), after cap verdict bytes
   static constexpr size_t arrays_off(uint32_t cap = kQcCap) {
@@ -157,6 +164,7 @@ struct ArmArgs {
   uint32_t halt;       // the mailbox's halt word at arming: any other value cancels
   uint64_t* relay;     // wide kernel (kQcCap waves): device word {number, n}, zeroed before launch; null: narrow
   uint32_t stamps;     // 1: each serving wave writes its GPU timestamps (pbftv_qc_stamps*; PBFTV_QC_STAMPS=1)
+  int slot;            // its armed stream slot: the expired word and live words it writes (QcMail)
 };
 hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st);
 

@@ -526,7 +526,7 @@ hipError_t qc_arm(Device& d) {
   }
   const char* se = getenv("PBFTV_QC_STAMPS");
   const ArmArgs a{qc_mail(d), want, qc_arm_budget(d.id), d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
-                  d.qptrs.as<const uint32_t* const>(), qc_spin(), halt, relay, se && se[0] == '1' ? 1u : 0u};
+                  d.qptrs.as<const uint32_t* const>(), qc_spin(), halt, relay, se && se[0] == '1' ? 1u : 0u, slot};
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = d.armed_first = want;
   d.arm_waves = relay ? kQcCap : QcMail::kQcSlots;
@@ -560,7 +560,7 @@ hipError_t qc_rotate(Device& d) {
 // retire the rotated-out kernel once its successor is resident
 void qc_retire(Device& d) {
   if (!d.retiring || !d.arm_seq) return;
-  const uint32_t* live = reinterpret_cast<const uint32_t*>(d.stage.as<uint8_t>() + QcMail::live_off());
+  const uint32_t* live = reinterpret_cast<const uint32_t*>(d.stage.as<uint8_t>() + QcMail::live_off(d.arm_stream));
   for (uint32_t w = 0; w < d.arm_waves; ++w)
     if (__atomic_load_n(live + w, __ATOMIC_ACQUIRE) != d.armed_first) return;  // not every wave resident yet
   __atomic_store_n(&qc_mail(d)->stop, d.retiring, __ATOMIC_RELEASE);
@@ -1707,7 +1707,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       return PBFTV_OK;
     };
     // an armed kernel that has left (budget, cancel, halt) is collected first
-    if (d.arm_seq && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == d.arm_seq) {
+    if (d.arm_seq && __atomic_load_n(m->expired(d.arm_stream), __ATOMIC_ACQUIRE) == d.arm_seq) {
       HIP_TRY(set_dev());
       HIP_TRY(qc_disarm(d));
     }
@@ -1768,7 +1768,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         if (++next == slots_n) h_slots = std::chrono::steady_clock::now();
         continue;
       }
-      if (cur && __atomic_load_n(&m->expired, __ATOMIC_ACQUIRE) == cur) {
+      if (cur && __atomic_load_n(m->expired(d.arm_stream), __ATOMIC_ACQUIRE) == cur) {
         // the armed kernel left (budget, cancel, halt) before it saw the bell:
         // wait for the armed kernels to leave, then launch
         HIP_TRY(set_dev());
@@ -1785,14 +1785,27 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
         // nothing that served (or could still serve) this call may outlive the
         // return: the armed kernels and the launched one have left after these
-        // synchronisations (a kernel fault surfaces here), so no stale verdict
-        // can land in the next call's result bytes
+        // synchronisations (a kernel fault surfaces here as a stream error), so
+        // no stale verdict can land in the next call's result bytes
         HIP_TRY(set_dev());
         HIP_TRY(qc_disarm(d));
         HIP_TRY(hipStreamSynchronize(d.stream));
-        for (uint64_t i = next; i < n; ++i)
-          if (res[i] == 0xFF) return fail(PBFTV_EDEVICE, "wave verify kernel did not report every signature");
-        break;
+        bool missing = false;
+        for (uint64_t i = next; i < n; ++i) missing |= res[i] == 0xFF;
+        if (!missing) break;
+        if (cur) {
+          // an armed server that left without its exit being seen (no fault:
+          // the streams synchronised cleanly) is a lost doorbell, not a device
+          // error: serve the request with a launch instead
+          cur = 0;
+          std::memset(const_cast<uint8_t*>(res), 0xFF, n);
+          int rc = launch_plain();
+          if (rc != PBFTV_OK) return rc;
+          next = 0;
+          t0 = std::chrono::steady_clock::now();
+          continue;
+        }
+        return fail(PBFTV_EDEVICE, "wave verify kernel did not report every signature");
       }
     }
     if (d.keeper_idle || (d.arm_seq == 0 && d.keeper.joinable())) {

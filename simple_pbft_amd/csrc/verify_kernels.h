@@ -1220,7 +1220,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
   uint32_t want = a.want;
   const uint64_t t0 = wall_clock64();
   // live: this wave is resident (a rotation retires the old kernel after all are)
-  if (lane == 0) reinterpret_cast<volatile uint32_t*>(base + QcMail::live_off())[b] = want;
+  if (lane == 0) reinterpret_cast<volatile uint32_t*>(base + QcMail::live_off(a.slot))[b] = want;
   // key data for keys < 128, two per lane (lane l: keys l and l + 64)
   const uint32_t nkeys = a.nkeys;
   const uint4* qt_lo = lane < nkeys ? reinterpret_cast<const uint4* const*>(a.qtabs)[lane] : nullptr;
@@ -1307,7 +1307,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
     if (!serve) {
       if (b == 0 && relay && lane == 0)  // the helpers leave with wave 0
         __hip_atomic_store(relay, ((uint64_t)0xFFFFFFFFu << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (lane == 0) __hip_atomic_store(&mail->expired, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane == 0) __hip_atomic_store(mail->expired(a.slot), want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
     const uint64_t seen_wall = wall_clock64(), seen_clk = clock64();

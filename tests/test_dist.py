@@ -100,3 +100,33 @@ def test_gloo_world2_sharded_verify_matches_single_process(ecdsa_fixtures):
     assert ok
     assert tmax == 2.0 and tsum == 2.0
     assert len(shards) == 2
+
+
+def _bench(args, env_extra, timeout=240):
+    import subprocess
+    env = dict(os.environ, PBFTV_BENCH_PROBE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("gpus", [1, 2, 3])
+def test_bench_gpus_flag_starts_that_many_ranks(gpus):
+    """`python bench.py --gpus N` (the driver's plain command, no torch.distributed.run)
+    starts N rank processes itself -- gloo barrier, max-over-ranks -- and the
+    ranks see WORLD_SIZE = N; --gpus 1 stays one process.  PBFTV_BENCH_PROBE
+    stops every rank right after the rendezvous, before any GPU call."""
+    import json
+    r = _bench(["--gpus", str(gpus), "--n", "4096"], {})
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["world_size"] == gpus and line["ranks_seen"] == gpus
+    assert line["spawned"] == (gpus > 1) and line["shared_data"] == (gpus > 1)
+
+
+def test_bench_gpus_mismatch_fails_loudly():
+    """Under torch.distributed.run with a world size other than --gpus, bench.py refuses."""
+    r = _bench(["--gpus", "2", "--n", "4096"], {"WORLD_SIZE": "1"})
+    assert r.returncode != 0 and "--gpus 2 but WORLD_SIZE=1" in r.stderr

@@ -579,9 +579,10 @@ def test_armed_latency_path(oracle_lib, mode, monkeypatch):
 
 def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypatch):
     """An armed kernel with a 5-s budget stays resident between calls.  A
-    device free, a pinned-host free, and another context's key change on the
-    same GPU (hipDeviceSynchronize) must not wait for it: the library quiesces
-    the GPU (halts every armed kernel on it) first.  The halted context's next
+    device free and a pinned-host free must not wait for it: the library
+    quiesces the GPU (halts every armed kernel on it) first.  Another
+    context's key change waits only for its OWN work (ctx_quiesce), so it does
+    not wait for context a's armed kernel either.  The halted context's next
     call falls back to a launch and is still right."""
     import time
     from simple_pbft_amd import Verifier
@@ -611,7 +612,7 @@ def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypa
             assert (a.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
             assert (b.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
         t0 = time.perf_counter()
-        assert b.set_key(1, keys[1])  # device synchronisation with a's kernel armed
+        assert b.set_key(1, keys[1])  # b's key change with a's kernel armed (b waits for b's work only)
         assert time.perf_counter() - t0 < 2.0
         for i in range(24, n_all - 3, 3):
             for v in (a, b):
@@ -702,3 +703,176 @@ def test_armed_exclusive_cu_option(oracle_lib, monkeypatch):
             o = rng.choice(n_all, 3, replace=False)
             assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all(), it
     assert armed >= 24, armed
+
+
+def _corrupted_certs(oracle_lib, per_cert, n_certs, seed, rng):
+    """n_certs certificates of per_cert votes by a 100-key committee (OpenSSL,
+    tools/synth.py), every one with 1-3 votes corrupted (a flipped bit of r, s
+    or the hash), so neither an all-accept nor an all-reject answer passes and
+    consecutive certificates differ in which votes fail.  Expected bits: oracle."""
+    import os
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth
+    pub, H, S, K = synth.certs(100, per_cert, n_certs, seed)
+    H = H.copy()
+    for c in range(n_certs):
+        for j in rng.choice(per_cert, int(rng.integers(1, min(3, per_cert - 1) + 1)), replace=False):
+            i = c * per_cert + int(j)
+            col = int(rng.integers(0, 96))
+            (S[i] if col < 64 else H[i])[col % 64 if col < 64 else col - 64] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    n = len(K)
+    bm = np.zeros((n + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(H.ctypes.data, S.ctypes.data, K.ctypes.data, n, pub.ctypes.data,
+                                              len(pub), bm.ctypes.data, 8)
+    want = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+    assert 0 < want.reshape(n_certs, per_cert).sum(1).min() and want.reshape(n_certs, per_cert).all(1).sum() == 0
+    return pub, [(H[c * per_cert:(c + 1) * per_cert], S[c * per_cert:(c + 1) * per_cert],
+                  K[c * per_cert:(c + 1) * per_cert], want[c * per_cert:(c + 1) * per_cert]) for c in range(n_certs)]
+
+
+@pytest.mark.parametrize("mode", ["keeper", "expiring"])
+def test_rekey_then_wide_certificates(oracle_lib, mode, monkeypatch):
+    """The sequence of round 4's on-hardware false reject (gpurun_out/r04a:
+    0 of 67 accepted on the first 67-signature certificate after a new key
+    set): register key set A (100 keys) -> 67-signature certificates, back to
+    back and after 1-s idle gaps -> register key set B (100 keys, same
+    geometry: the key-table slots are reused in place) -> 3-signature
+    certificates served armed -> 67- and 129-signature certificates -> 3 again.
+    Every certificate carries corrupted votes; every bitmap against the oracle,
+    and each quorum count.  "expiring": no keeper and a 300-ms budget, so the
+    1-s gaps find the armed kernel gone (the round-3 library's behaviour at
+    the reference's tick)."""
+    import time
+    from simple_pbft_amd import Verifier
+    if mode == "expiring":
+        monkeypatch.setenv("PBFTV_QC_KEEP_MS", "0")
+        monkeypatch.setenv("PBFTV_QC_ARM_MS", "300")
+    rng = np.random.default_rng(505)
+    pubA, a67 = _corrupted_certs(oracle_lib, 67, 24, 201, rng)
+    pubB, b3 = _corrupted_certs(oracle_lib, 3, 70, 0x50424654, rng)
+    pubB2, b67 = _corrupted_certs(oracle_lib, 67, 30, 0x50424654, rng)
+    assert (pubB == pubB2).all() and not (pubA == pubB).all()
+    # 129 signatures (past the armed kernel's 128 waves): two certificates' votes in one call
+    b129 = [tuple(np.concatenate([x[j], y[j][:62]]) for j in range(4)) for x, y in zip(b67[24::2], b67[25::2])]
+    b67 = b67[:24]
+    bad = []
+    armed = {"b3": 0}
+
+    def serve(v, label, calls, gap=0.0):
+        for i, (H, S, K, want) in enumerate(calls):
+            if gap:
+                time.sleep(gap)
+            bm, acc, ok = v.qc_verify(H, S, K, quorum=len(K))
+            if not ((bm == want).all() and acc == int(want.sum()) and not ok):
+                bad.append((label, i, len(K), int(acc), int(want.sum())))
+            if label.startswith("B3"):
+                armed["b3"] += v.qc_stamps(0)["armed"]
+
+    with Verifier(device_mask=1) as v:
+        v.register_keys(pubA)
+        serve(v, "A67", a67[:20])
+        serve(v, "A67_tick", a67[20:22], gap=1.0)
+        serve(v, "A67_after", a67[22:])
+        time.sleep(0.5)
+        v.register_keys(pubB)
+        serve(v, "B3", b3[:20])
+        serve(v, "B3_gap2ms", b3[20:60], gap=0.002)
+        serve(v, "B67", b67)
+        serve(v, "B129", b129)
+        serve(v, "B3_after", b3[60:])
+    assert not bad, bad[:10]
+    assert armed["b3"] >= 50, armed  # the 3-signature certificates were served by the armed kernel
+
+
+def test_external_device_sync_bounded_by_budget(oracle_lib, monkeypatch):
+    """A hipDeviceSynchronize made OUTSIDE the library (the caller's own HIP
+    code) while the keeper holds an armed kernel on the GPU waits for that
+    kernel: the wait is bounded by its budget (PBFTV_QC_ARM_MS; the keeper
+    rotates at half of it), documented as ~1.5 budgets.  With a 200-ms budget
+    the sync must return within 2 budgets plus slack, and later certificates
+    are still served right."""
+    import ctypes
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", "200")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=4, per_key=12, seed=83)
+    sigs[::4, 33] ^= 0x02
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    hip = ctypes.CDLL("libamdhip64.so")  # the runtime libpbftv.so already loaded (same soname)
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        waits = []
+        for rep in range(3):
+            for i in range(0, 12, 3):
+                assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
+            assert v.qc_stamps(0)["armed"]
+            time.sleep(0.03 * rep)
+            t0 = time.perf_counter()
+            assert hip.hipDeviceSynchronize() == 0
+            waits.append(time.perf_counter() - t0)
+        assert max(waits) < 2 * 0.2 + 0.15, waits
+        for i in range(12, n_all - 3, 3):
+            assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all(), i
+
+
+def test_quiesce_during_rotations(oracle_lib, monkeypatch):
+    """a quiesce (another context's device free bumps the halt word
+    of every mailbox on the GPU) can land while a rotation has two armed
+    kernels resident; both leave at once.  Each armed stream slot has its own
+    expired word, so the owner sees its CURRENT kernel's exit and serves the
+    next certificate with a launch instead of ringing a kernel that is gone.
+    A 40-ms budget makes the keeper rotate every 20 ms while a second context
+    frees device memory in a loop: every certificate right, none slow."""
+    import threading
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", "40")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=5, per_key=40, seed=87)
+    sigs[::6, 21] ^= 0x40
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    stop = threading.Event()
+    frees = [0]
+    with Verifier(device_mask=1) as a, Verifier(device_mask=1) as b:
+        a.register_keys(keys)
+
+        def freer():
+            while not stop.is_set():
+                buf = b.alloc(0, 1 << 16)
+                buf.free()
+                frees[0] += 1
+                time.sleep(0.003)
+        th = threading.Thread(target=freer)
+        th.start()
+        rng = np.random.default_rng(88)
+        slow, wrong = [], []
+        try:
+            t_end = time.perf_counter() + 3.0
+            it = 0
+            while time.perf_counter() < t_end:
+                m = int(rng.choice([1, 3, 4, 8, 67]))
+                o = rng.choice(n_all, m, replace=False)
+                t0 = time.perf_counter()
+                got = a.verify_batch(hashes[o], sigs[o], kidx[o])
+                dt = time.perf_counter() - t0
+                if dt > 0.5:
+                    slow.append((it, m, dt))
+                if not (got == want[o]).all():
+                    wrong.append((it, m))
+                it += 1
+                time.sleep(float(rng.choice([0.0, 0.005, 0.02])))
+        finally:
+            stop.set()
+            th.join()
+    assert not wrong, wrong[:5]
+    assert not slow, slow[:5]
+    assert frees[0] > 100 and it > 100, (frees[0], it)
