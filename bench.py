@@ -141,6 +141,38 @@ def dist_env():
     return ws, rank, local
 
 
+def register_with_phases(ver, pub):
+    """pbftv_register_keys timed, with its per-phase wall times: the library's
+    PBFTV_TRACE lines (pbftv_api.cpp trace(): quiesce, geometry, release old key
+    tables, G table allocation / build, key table allocation / build, and inside
+    each build its table scratch and table kernels) read from this process's
+    stderr for the duration of the call.  PBFTV_TRACE is set by main() before
+    the first registration (the library reads it once)."""
+    import re
+    import tempfile
+    sys.stderr.flush()
+    saved = os.dup(2)
+    with tempfile.TemporaryFile() as f:
+        os.dup2(f.fileno(), 2)
+        try:
+            t0 = time.perf_counter()
+            valid = ver.register_keys(pub)
+            wall = time.perf_counter() - t0
+        finally:
+            os.dup2(saved, 2)
+            os.close(saved)
+        f.seek(0)
+        text = f.read().decode(errors="replace")
+    phases = {}
+    for line in text.splitlines():
+        m = re.match(r"pbftv\[dev (\d+)\] (.+): ([0-9.]+) ms$", line)
+        if m:
+            phases[m.group(2)] = round(phases.get(m.group(2), 0.0) + float(m.group(3)), 1)
+        elif line:
+            sys.stderr.write(line + "\n")
+    return valid, wall, phases
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -244,9 +276,8 @@ def in_context_leg(ws: int, share: bool, pub, H, S, K, ok, steps: int, warmup_ms
         H, S, K = (np.ascontiguousarray(a) for a in (H, S, K))
         ok = np.asarray(ok, bool)
         n = len(K)
-        t = time.perf_counter()
-        valid = ver.register_keys(np.ascontiguousarray(pub))
-        out["registration_wall_s"] = time.perf_counter() - t
+        valid, out["registration_wall_s"], out["registration_phases_ms"] = register_with_phases(
+            ver, np.ascontiguousarray(pub))
         assert valid.all()
         gb, qb, tb = ver.table_config()
         out["comb_window_bits"] = {"G": gb, "keys": qb}
@@ -935,6 +966,7 @@ def main():
                 import shutil
                 shutil.rmtree(dd, ignore_errors=True)
         sys.exit(rc)
+    os.environ.setdefault("PBFTV_TRACE", "1")  # registration phases (register_with_phases)
     if args.gpus != ws:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} rank processes: launch with "
                          f"--nproc-per-node {args.gpus}, or without torch.distributed.run")
@@ -977,14 +1009,10 @@ def main():
     if share:  # ranks sharing one GPU register one after the other: each sizes its tables from what is free
         for r in range(ws):
             if r == rank:
-                t_reg = time.perf_counter()
-                valid = ver.register_keys(pub)
-                t_reg = time.perf_counter() - t_reg
+                valid, t_reg, reg_phases = register_with_phases(ver, pub)
             d.barrier()
     else:
-        t_reg = time.perf_counter()
-        valid = ver.register_keys(pub)
-        t_reg = time.perf_counter() - t_reg  # G table + one table per key, built on the device
+        valid, t_reg, reg_phases = register_with_phases(ver, pub)  # G table + one table per key, built on the device
     assert valid.all()
     dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
     ver.reserve(n)
@@ -1121,7 +1149,10 @@ def main():
                                                 "source": "tools/gather_comb.hip, profiles/r03_gather_comb.txt"}
         out["kernels"] = kern
         out["config"]["comb_window_bits"] = {"G": gb, "keys": qb, "table_bytes_per_gpu": tb}
-        out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "what": "pbftv_register_keys: G table + the key tables built on the device (incl. allocation)"}
+        out["registration_s"] = {"keys": args.keys, "wall_s": t_reg, "phases_ms": reg_phases,
+                                 "what": "pbftv_register_keys: G table + the key tables built on the device (incl. "
+                                         "allocation); phases_ms from the library's PBFTV_TRACE (the table scratch / "
+                                         "table kernels lines are the parts of each build)"}
         if not args.no_extras and ws == 1:
             # host-buffer path with no armed latency kernel on the GPU (none armed yet)
             out["host_path"] = host_path(ver, H, S, K, ok)

@@ -218,6 +218,10 @@ struct Device {
   // diagnostics of the last latency-path call (pbftv_qc_stamps)
   uint64_t qc_ns_entry = 0, qc_ns_handover = 0, qc_ns_total = 0, qc_ns_slots = 0;
   char hot_end[1] = {};
+  // when the lane-path batches enqueued so far are expected to finish
+  // (steady-clock ns; an estimate from their sizes, kept without a HIP call):
+  // a multi-device context sends a certificate to its least-loaded device
+  std::atomic<int64_t> busy_until_ns{0};
   // signature state: comb table of G (width gbits) and one table per registered
   // key (width qbits), addressed through qptrs (device array, by key).  Key
   // tables live in blocks (one per registration / add_keys call; slots beyond
@@ -1322,6 +1326,7 @@ static int register_tables(Device& d, const std::vector<uint32_t>& le, uint32_t 
     auto it = g_tables.find({dev_id, g});
     return it != g_tables.end() && !it->second.tab.expired();  // ours or another context's: no new HBM
   });
+  trace("geometry", d.id, t0);
   d.nkeys = 0;
   if (wq != d.qbits || d.qtab.size() < k) {  // new width or too few slots: new blocks (freeing HBM
     for (auto& b : d.qblocks) b->release();  // the driver wipes is slow: same-width re-registrations
@@ -1378,6 +1383,7 @@ int pbftv_register_keys(pbftv_ctx* ctx, const uint8_t* pub_xy, uint32_t k, uint8
     // call rewrites in place: its armed kernels, its streams and the caller
     // streams it was given (a verify enqueued on one with *_dev)
     HIP_TRY(ctx_quiesce(d));
+    trace("quiesce", d.id, t0);
     d.have_keys = false;
     // another process or context can take HBM between the free-memory query
     // and the allocations: on ENOMEM this device's tables are freed and the
@@ -1468,6 +1474,39 @@ int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uin
 // Lane path (or the one-wave-per-signature path for small n) of one batch on
 // stream st.  own == nullptr: the device's shared scratch, ordered across
 // streams by the scratch event; else the caller's (a pipeline stream's own).
+static int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// a lane-path batch of n signatures was enqueued on d: ~1.1 ns per signature
+// of device time (the 1M step), queued behind what is already there
+static void note_busy(Device& d, uint64_t n) {
+  const int64_t now = steady_ns(), add = (int64_t)(1.1 * (double)n) + 20000;
+  int64_t cur = d.busy_until_ns.load(std::memory_order_relaxed);
+  while (!d.busy_until_ns.compare_exchange_weak(cur, std::max(cur, now) + add, std::memory_order_relaxed)) {
+  }
+}
+
+// the device a latency-path call goes to: devs[0] unless it is busy with
+// lane-path batches and another device is less so (an idle device with an
+// armed server first, then the earliest-free one)
+static Device* latency_device(pbftv_ctx* ctx) {
+  Device* best = ctx->dev0;
+  if (ctx->devs.size() == 1) return best;
+  const int64_t now = steady_ns();
+  int64_t best_free = std::max<int64_t>(best->busy_until_ns.load(std::memory_order_relaxed), now);
+  if (best_free <= now) return best;
+  for (auto& dp : ctx->devs) {
+    const int64_t f = std::max<int64_t>(dp->busy_until_ns.load(std::memory_order_relaxed), now);
+    if (f < best_free || (f == best_free && f <= now && dp->arm_seq && !best->arm_seq)) {
+      best = dp.get();
+      best_free = f;
+    }
+  }
+  return best;
+}
+
 static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d_sigs, const uint32_t* d_key_idx,
                             uint64_t n, uint8_t* d_bitmap, hipStream_t st, VerifyScratch* own = nullptr) {
   if (!d.have_keys) return fail(PBFTV_ENOKEYS, "pbftv_register_keys has not been called");
@@ -1484,6 +1523,7 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
     if (it != d.stream_scratch.end()) own = it->second.get();
   }
   VerifyScratch& sc = own ? *own : d.vs;
+  note_busy(d, n);
   HIP_TRY(sc.rec.ensure(pbftv::ecdsa_record_bytes(n)));
   HIP_TRY(sc.prefix.ensure(pbftv::scalar_prefix_bytes(n)));
   if (!own) HIP_TRY(scratch_acquire(d, st));
@@ -1627,14 +1667,15 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
   const auto h_entry = std::chrono::steady_clock::now();
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
   if (n && (!hashes || !sig_rs || !key_idx || !out_bitmap)) return fail(PBFTV_EINVAL, "null buffer");
-  if (n && n <= QcMail::kQcCap && ctx->dev0) {
+  Device* const ldev = n && ctx->dev0 ? latency_device(ctx) : nullptr;
+  if (n && n <= QcMail::kQcCap && ldev) {
     // A certificate after an idle second finds this core's caches cold (the
     // caller slept; its core's private caches were flushed): start the misses
     // of the lines the armed path touches now, in parallel, instead of one
     // after another (device lock and state, the mailbox header, slot lines and
     // verdict bytes: the mailbox's first page).  A stale mailbox pointer is
     // harmless: a prefetch never faults.
-    const Device* d0 = ctx->dev0;
+    const Device* d0 = ldev;
     for (const char* q = reinterpret_cast<const char*>(&d0->mu); q <= d0->hot_end; q += 64) __builtin_prefetch(q, 1, 3);
     __builtin_prefetch(d0->hot_end, 1, 3);
     if (const uint8_t* mb = static_cast<const uint8_t*>(d0->stage.p)) {
@@ -1667,8 +1708,9 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     // device (qc_arm, qc_keeper_loop): the request writes its slot lines and
     // rings, and nothing else -- no launch, no HIP call -- is on its path.
     // Otherwise, or when the armed kernel has run out, one launch of
-    // k_ecdsa_wave (up to 2048 signatures, one wave each).
-    Device& d = *ctx->dev0;
+    // k_ecdsa_wave (up to 2048 signatures, one wave each).  In a multi-device
+    // context the call goes to the least-loaded device (latency_device).
+    Device& d = *ldev;
     std::lock_guard<std::mutex> lk(d.mu);
     const auto h_in = std::chrono::steady_clock::now();
     d.last_qc = h_in;

@@ -198,13 +198,17 @@ __device__ __forceinline__ const uint4* entry_ptr(const uint4* __restrict__ tab,
 // Async copy of this lane's 64-B entry into sent[.][t]: four 16-B
 // global_load_lds, each writing the wave's 64 lanes contiguously at the
 // wave-uniform base &sent[k][t & ~63].
+// PBFTV_GATHER_AUX: the loads' cache-policy bits (experiment builds; 2 = nt)
+#ifndef PBFTV_GATHER_AUX
+#define PBFTV_GATHER_AUX 0
+#endif
 __device__ __forceinline__ void issue_entry_lds(uint4 (*sent)[PBFTV_COMB_BLOCK], uint32_t t, const uint4* p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this lane's reads of the slot are done
   const uint32_t wb = t & ~63u;
-  __builtin_amdgcn_global_load_lds(p + 0, &sent[0][wb], 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(p + 1, &sent[1][wb], 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(p + 2, &sent[2][wb], 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(p + 3, &sent[3][wb], 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(p + 0, &sent[0][wb], 16, 0, PBFTV_GATHER_AUX);
+  __builtin_amdgcn_global_load_lds(p + 1, &sent[1][wb], 16, 0, PBFTV_GATHER_AUX);
+  __builtin_amdgcn_global_load_lds(p + 2, &sent[2][wb], 16, 0, PBFTV_GATHER_AUX);
+  __builtin_amdgcn_global_load_lds(p + 3, &sent[3][wb], 16, 0, PBFTV_GATHER_AUX);
 }
 
 __device__ __forceinline__ void read_entry_lds(uint4 (*sent)[PBFTV_COMB_BLOCK], uint32_t t, uint32_t ew[16]) {
@@ -1350,12 +1354,17 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
 
 template <int WG, int WQ>
 void launch_armed_w(const ArmArgs& a, hipStream_t st) {
-  // PBFTV_QC_EXCLUSIVE_CU=1 (opt-in): every armed workgroup takes its CU's
-  // whole LDS, so no other kernel's block shares a CU -- and a SIMD's issue
-  // slots -- with the armed waves (a certificate under a concurrent batch);
-  // the batch then runs on the other CUs.  Read at every arming.
+  // Whole CUs for the armed waves: an armed workgroup that takes its CU's
+  // whole LDS shares no CU -- and no SIMD issue slots -- with a concurrent
+  // batch's blocks; the batch runs on the other CUs.  PBFTV_QC_EXCLUSIVE_CU
+  // (read at every arming): "narrow" (the default) for the 8-wave kernel
+  // only -- 2 CUs of 256 (<1 % of a batch's CUs) for a certificate of up to
+  // 8 signatures that no batch slows -- "1" for the wide kernel too (32
+  // CUs), "0" for neither.
   const char* e = getenv("PBFTV_QC_EXCLUSIVE_CU");
-  const uint32_t lds = e && e[0] == '1' ? 160u * 1024u : 0u;
+  const bool wide = a.relay != nullptr;
+  const bool excl = e ? (e[0] == '1' || (!wide && e[0] == 'n')) : !wide;
+  const uint32_t lds = excl ? 160u * 1024u : 0u;
   if (lds) {
     static bool attr = false;  // (per instantiation)
     if (!attr) {

@@ -236,3 +236,44 @@ def test_bitmap_padding_bits_are_zero(oracle_lib, monkeypatch):
             assert rc == 0
             bits = np.unpackbits(bm[:(n + 7) // 8], bitorder="little")
             assert bits[:n].all() and not bits[n:].any(), n
+
+
+def test_latency_path_goes_to_least_loaded_device(oracle_lib, monkeypatch):
+    """in a multi-device context a certificate goes to the
+    device with the least lane-path work queued (pbftv_api.cpp
+    latency_device), not always to device 0.  Two logical devices on GPU 0
+    (PBFTV_ALIAS_DEVICES=2): with a 1M batch just enqueued on device 0, the
+    next certificate is served on device 1 (its pbftv_qc_stamps record the
+    call); with nothing queued it goes to device 0.  Every bitmap against the
+    oracle."""
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_ALIAS_DEVICES", "2")
+    monkeypatch.setenv("PBFTV_GBITS", "24")
+    monkeypatch.setenv("PBFTV_QBITS", "16")
+    keys, H, S, K = oracle_sign_pool(oracle_lib, 4, 16, seed=73)
+    S[::5, 11] ^= 0x10
+    want = _oracle_bits(oracle_lib, H, S, K, keys)
+    n = 1 << 20
+    reps = n // len(K)
+    with Verifier(device_mask=1) as v:
+        assert v.device_count() == 2
+        v.register_keys(keys)
+        dh, ds, dk = (v.to_device(0, np.tile(a, (reps, 1)) if a.ndim > 1 else np.tile(a, reps)) for a in (H, S, K))
+        db = v.alloc(0, n // 8 + 1)
+        try:
+            for i in range(0, 12, 3):  # idle: device 0 serves
+                assert (v.verify_batch(H[i:i + 3], S[i:i + 3], K[i:i + 3]) == want[i:i + 3]).all()
+            before = v.qc_stamps(1)["total_us"]
+            assert v.qc_stamps(0)["total_us"] > 0 and before == 0
+            time.sleep(0.01)
+            v.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)  # ~1 ms of device 0 queued
+            got = v.verify_batch(H[12:15], S[12:15], K[12:15])
+            assert (got == want[12:15]).all()
+            assert v.qc_stamps(1)["total_us"] > 0  # served by device 1
+            v.sync(0)
+            bm = np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool)
+            assert (bm == np.tile(want, reps)).all()
+        finally:
+            for b in (dh, ds, dk, db):
+                b.free()
