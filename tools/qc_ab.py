@@ -1,6 +1,6 @@
 """Same-box A/B of the latency path: p50 of pbftv_qc_verify (one n = 4
 certificate of 3 signatures, pre-marshalled call) for the library given by
-PBFTV_LIB.  tools/qc_ab.sh alternates builds.  Prints one JSON line."""
+PBFTV_LIB.  tools/ab.sh (workload qc) alternates builds.  Prints one JSON line."""
 import json
 import os
 import sys
