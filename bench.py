@@ -458,7 +458,12 @@ def qc_under_load(ver: Verifier, dh, ds, dk, n: int, ok, seed: int, calls3: int 
     same context (a background thread enqueues two batches, waits, repeats):
     what a certificate costs while the node also drains a large pool snapshot.
     Certificates are signed by the registered config-4 committee (its keys:
-    synth.certs with the same seed)."""
+    synth.certs with the same seed).  A node sees ONE certificate size (its
+    committee's), so the sizes are measured one after the other, each in the
+    state its own calls leave: 3 signatures (n = 4) idle then loaded -- the
+    8-wave armed kernel, whole CUs -- then 67 (n = 100) idle then loaded -- the
+    128-wave kernel.  The stream's rate alone (no certificate, nothing armed
+    yet) is measured first, for the ratio."""
     import threading
     _, H3, S3, K3 = synth.certs(100, 3, 2 * calls3 + 40, seed)
     _, H67, S67, K67 = synth.certs(100, 67, 2 * calls67 + 20, seed)
@@ -466,30 +471,45 @@ def qc_under_load(ver: Verifier, dh, ds, dk, n: int, ok, seed: int, calls3: int 
     def part(H, S, K, sigs, lo, cnt):
         sl = slice(lo * sigs, (lo + cnt + 10) * sigs)
         return qc_latency(ver, 100, sigs, cnt, 0, gap_s=0.002, warm=10, certs=(H[sl], S[sl], K[sl]))
-    out = {"idle_3sigs": part(H3, S3, K3, 3, 0, calls3), "idle_67sigs": part(H67, S67, K67, 67, 0, calls67)}
     st = ver.stream_create(0)
     db = ver.alloc(0, n // 8 + 1)
-    stop = threading.Event()
-    done = [0]
 
-    def stream():
-        while not stop.is_set():
-            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr, stream=st)
-            ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr, stream=st)
-            ver.stream_wait(0, st)
-            done[0] += 2
-    th = threading.Thread(target=stream)
-    th.start()
-    try:
-        time.sleep(0.05)
-        t0 = time.perf_counter()
-        b0 = done[0]
-        out["loaded_3sigs"] = part(H3, S3, K3, 3, calls3 + 20, calls3)
-        out["loaded_67sigs"] = part(H67, S67, K67, 67, calls67 + 10, calls67)
-        out["stream_verifies_per_s_during"] = (done[0] - b0) * n / (time.perf_counter() - t0)
-    finally:
-        stop.set()
-        th.join()
+    def loaded(fn):
+        """fn() while the stream runs; returns (fn's result, stream verifies/s meanwhile)"""
+        stop = threading.Event()
+        done = [0]
+
+        def stream():
+            while not stop.is_set():
+                ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr, stream=st)
+                ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr, stream=st)
+                ver.stream_wait(0, st)
+                done[0] += 2
+        th = threading.Thread(target=stream)
+        th.start()
+        try:
+            time.sleep(0.05)
+            t0 = time.perf_counter()
+            b0 = done[0]
+            r = fn()
+            rate = (done[0] - b0) * n / (time.perf_counter() - t0)
+        finally:
+            stop.set()
+            th.join()
+        return r, rate
+    out = {}
+    _, out["stream_verifies_per_s_alone"] = loaded(lambda: time.sleep(0.6))
+    out["idle_3sigs"] = part(H3, S3, K3, 3, 0, calls3)
+    out["loaded_3sigs"], r3 = loaded(lambda: part(H3, S3, K3, 3, calls3 + 20, calls3))
+    # the stream again with the 8-wave kernel armed (the keeper holds it) and no certificate
+    _, out["stream_verifies_per_s_armed_narrow"] = loaded(lambda: time.sleep(0.6))
+    out["idle_67sigs"] = part(H67, S67, K67, 67, 0, calls67)
+    out["loaded_67sigs"], r67 = loaded(lambda: part(H67, S67, K67, 67, calls67 + 10, calls67))
+    out["stream_verifies_per_s_during"] = {"3sigs": r3, "67sigs": r67}
+    out["stream_rate_ratio"] = {"3sigs": r3 / out["stream_verifies_per_s_alone"],
+                                "67sigs": r67 / out["stream_verifies_per_s_alone"],
+                                "armed_narrow_no_calls": out["stream_verifies_per_s_armed_narrow"] /
+                                out["stream_verifies_per_s_alone"]}
     out["stream_check"] = bool((np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool) == ok).all())
     db.free()
     ver.stream_destroy(0, st)

@@ -112,11 +112,17 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
  *   PBFTV_QC_KEEP_MS=10000    keep one armed this long after the last call
  *                             (0: no keeper; the kernel runs out);
  *   PBFTV_QC_WIDE=0           never arm the 128-wave form;
+ *   PBFTV_QC_YIELD=1          no armed kernel while lane-path batches
+ *                             run: a batch enqueue halts it, certificates
+ *                             meanwhile are launched (slower beside the
+ *                             batch), the keeper re-arms after it.  Any
+ *                             resident kernel slows a busy stream by 3-7 %
+ *                             on this hardware; off by default;
  *   PBFTV_QC_EXCLUSIVE_CU     armed workgroups take whole CUs, so a
- *                             concurrent batch does not share their SIMDs:
- *                             "narrow" (default) the 8-wave kernel only (2
- *                             CUs), "1" the 128-wave kernel too (32 CUs, a
- *                             few % of a concurrent batch's rate), "0" none;
+ *                             concurrent batch does not share their SIMDs
+ *                             (with PBFTV_QC_YIELD=0): "narrow" the 8-wave
+ *                             kernel (2 CUs), "1" the 128-wave one too (32
+ *                             CUs); off by default;
  *   PBFTV_QC_STAMPS=1         the kernel records GPU timestamps
  *                             (pbftv_qc_stamps*).
  * pbftv_dev_free / pbftv_host_free and the library's own frees stop every

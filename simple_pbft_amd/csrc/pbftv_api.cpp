@@ -238,6 +238,7 @@ struct Device {
   VerifyScratch vs;  // the lane path's stage-1 records, prefix products, key order, result bytes
   // the armed kernels' streams, relay words and keeper thread
   hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: a rotation's successor spins beside its predecessor
+  hipStream_t lstream = nullptr;  // launched latency-path kernels: never queued behind a batch on d.stream
   DevBuf qrelay;                           // the wide kernels' relay words, one 64-B line per qstream:
                                            // uncached device memory (read and written past the 8 XCDs' L2s, so
                                            // no cache maintenance: an agent-scope acquire per poll would
@@ -400,6 +401,28 @@ uint32_t qc_spin() {
   return e ? (uint32_t)atoi(e) : 0u;
 }
 
+// PBFTV_QC_YIELD=1 (opt-in): no armed kernel stays resident while lane-path
+// batches are queued on its device.  Any kernel resident on another queue
+// slows a busy stream's kernels by 3-7 % on this hardware, even one that only
+// sleeps (tools/persist_cost.hip, profiles/r05_persist_cost.txt), so a
+// certificate server armed beside a large flush costs the flush that much.
+// With yield, a batch enqueue halts the armed kernel, a certificate in the
+// meantime is served by a launch on the latency stream, and the keeper arms
+// again once the queued batches are expected to be done.  Off by default: a
+// certificate launched beside a batch waits for free wave slots (~0.28 ms
+// instead of ~0.055 ms armed, profiles/r05_qc_yield_ab.txt).
+bool qc_yield() {
+  const char* e = getenv("PBFTV_QC_YIELD");
+  return e && e[0] == '1';
+}
+
+int64_t steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+bool lane_busy(const Device& d) { return d.busy_until_ns.load(std::memory_order_relaxed) > steady_ns(); }
+
 QcMail* qc_mail(Device& d) { return d.stage.as<QcMail>(); }
 
 // the mailbox enters the process-wide registry (so a quiesce of its GPU halts
@@ -459,7 +482,7 @@ hipError_t qc_disarm(Device& d) {
 // table).  Frees inside the key change still quiesce the GPU (DevBuf).
 hipError_t ctx_quiesce(Device& d) {
   HIP_TRY_E(qc_disarm(d));
-  for (hipStream_t s : {d.stream, d.stream2, d.cstream})
+  for (hipStream_t s : {d.stream, d.stream2, d.cstream, d.lstream})
     if (s) HIP_TRY_E(hipStreamSynchronize(s));
   for (auto& kv : d.stream_scratch) HIP_TRY_E(hipStreamSynchronize(kv.first));
   if (d.scratch_st && d.scratch_st != d.stream && d.scratch_ev) HIP_TRY_E(hipEventSynchronize(d.scratch_ev));
@@ -506,9 +529,21 @@ bool qc_wide_wanted(const Device& d) {
 // a quiesce of this GPU is in progress: the request then takes a launch).
 hipError_t qc_arm(Device& d) {
   if (d.arm_seq || !qc_arm_enabled() || !d.have_keys) return hipSuccess;
+  if (qc_yield() && lane_busy(d)) return hipSuccess;  // the keeper arms once the batches are done
   HIP_TRY_E(qc_mail_ready(d));
-  for (hipStream_t& q : d.qstream)
-    if (!q) HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+  // The armed kernels' streams have the HIGHEST priority: HIP keeps
+  // high-priority streams on hardware queues of their own, and a kernel that
+  // stays resident on a normal-priority queue makes every synchronous
+  // null-stream operation on the GPU (hipMemcpy, a caller's or this
+  // library's) wait until it ends -- a full budget (tools/queue_share.hip,
+  // profiles/r05_queue_share.txt).  The CP also dispatches them first.
+  for (hipStream_t& q : d.qstream) {
+    if (q) continue;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi) != hipSuccess)
+      HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+  }
   uint32_t halt;
   {
     // the check and the halt snapshot in one critical section: a quiesce that
@@ -584,7 +619,11 @@ void qc_keeper_loop(Device* d) {
     const auto keep = std::chrono::microseconds((int64_t)(qc_keep_ms() * 1000.0));
     auto wake = now + far;
     qc_retire(*d);
-    if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
+    const int64_t busy_ns = d->busy_until_ns.load(std::memory_order_relaxed) - steady_ns();
+    if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep && qc_yield() && busy_ns > 0) {
+      // lane-path batches are queued: nothing armed until they are expected done
+      wake = now + std::chrono::nanoseconds(busy_ns + 50000);
+    } else if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
       // also re-arms after a disarm (key change) or a halt (quiesce)
       const bool reshape = d->arm_seq && (d->arm_waves == kQcCap) != qc_wide_wanted(*d);
       if (d->arm_seq == 0 || now >= d->armed_at + half || reshape) {
@@ -911,6 +950,10 @@ void pbftv_close(pbftv_ctx* ctx) {
     if (d->stream2) {
       (void)hipStreamSynchronize(d->stream2);
       (void)hipStreamDestroy(d->stream2);
+    }
+    if (d->lstream) {
+      (void)hipStreamSynchronize(d->lstream);
+      (void)hipStreamDestroy(d->lstream);
     }
     d->vs2.release();
     for (auto& kv : d->stream_scratch) {  // streams the caller did not destroy: their scratch
@@ -1474,17 +1517,20 @@ int pbftv_table_config(const pbftv_ctx* ctx, int* out_gbits, int* out_qbits, uin
 // Lane path (or the one-wave-per-signature path for small n) of one batch on
 // stream st.  own == nullptr: the device's shared scratch, ordered across
 // streams by the scratch event; else the caller's (a pipeline stream's own).
-static int64_t steady_ns() {
-  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
-
-// a lane-path batch of n signatures was enqueued on d: ~1.1 ns per signature
-// of device time (the 1M step), queued behind what is already there
-static void note_busy(Device& d, uint64_t n) {
-  const int64_t now = steady_ns(), add = (int64_t)(1.1 * (double)n) + 20000;
+// a lane-path batch of n signatures was enqueued on d: ~ns_per_sig of device
+// time per signature (1.1: the device-resident 1M step; the host-buffer path
+// is PCIe-bound at ~2.3), queued behind what is already there.  With
+// PBFTV_QC_YIELD an armed kernel of d is halted now (it leaves at its next
+// poll; a certificate meanwhile takes a launch) -- d.mu is held.
+static void note_busy(Device& d, uint64_t n, double ns_per_sig = 1.1) {
+  const int64_t now = steady_ns(), add = (int64_t)(ns_per_sig * (double)n) + 20000;
   int64_t cur = d.busy_until_ns.load(std::memory_order_relaxed);
   while (!d.busy_until_ns.compare_exchange_weak(cur, std::max(cur, now) + add, std::memory_order_relaxed)) {
+  }
+  if (qc_yield() && d.arm_seq && d.stage.p && d.mail_registered) {
+    __atomic_add_fetch(&qc_mail(d)->halt, 1u, __ATOMIC_RELEASE);
+    d.arm_seq = 0;
+    d.retiring = 0;
   }
 }
 
@@ -1597,6 +1643,7 @@ static int verify_host_pipelined(Device& d, const uint8_t* H, const uint8_t* S, 
                                  uint8_t* out_bm) {
   const std::vector<uint64_t> chunks = host_chunks(m);
   const uint64_t c = *std::max_element(chunks.begin(), chunks.end()), nch = chunks.size();
+  note_busy(d, m, 1.2);  // the PCIe-bound part beyond the chunks' own verify time (~2.3 ns per signature in all)
   const int ns = (int)std::min<uint64_t>(nch, host_slots());
   const size_t oh = 0, os = 32 * c, ok = 96 * c, slot = 100 * c;  // slot layout: hashes | sigs | keys
   // every key index in one copy up front (one DMA command per chunk fewer;
@@ -1741,10 +1788,11 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       std::memcpy(sp, sig_rs, 64 * n);
       std::memcpy(kp, key_idx, 4 * n);
       HIP_TRY(set_dev());
-      HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.stream, [&] {
+      if (!d.lstream) HIP_TRY(hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking));
+      HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.lstream, [&] {
         return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n, d.key_valid.as<uint32_t>(), d.nkeys,
                                         d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,
-                                        const_cast<uint8_t*>(res), d.stream);
+                                        const_cast<uint8_t*>(res), d.lstream);
       }));
       return PBFTV_OK;
     };
@@ -1831,7 +1879,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         // no stale verdict can land in the next call's result bytes
         HIP_TRY(set_dev());
         HIP_TRY(qc_disarm(d));
-        HIP_TRY(hipStreamSynchronize(d.stream));
+        if (d.lstream) HIP_TRY(hipStreamSynchronize(d.lstream));
         bool missing = false;
         for (uint64_t i = next; i < n; ++i) missing |= res[i] == 0xFF;
         if (!missing) break;

@@ -1303,6 +1303,8 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
         break;  // header stop / halt, or the budget
       if (a.spin == 0) {
         __builtin_amdgcn_s_sleep(2);
+      } else if (a.spin >= 1000) {  // (experiments) (spin - 1000) x s_sleep(8) between polls
+        for (uint32_t j = 1000; j < a.spin; ++j) __builtin_amdgcn_s_sleep(8);
       } else if (a.spin > 1) {
         uint32_t x = lane;
         for (uint32_t j = 0; j < a.spin; ++j) asm volatile("v_mad_u32_u24 %0, %0, %0, %0" : "+v"(x));
@@ -1354,16 +1356,16 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
 
 template <int WG, int WQ>
 void launch_armed_w(const ArmArgs& a, hipStream_t st) {
-  // Whole CUs for the armed waves: an armed workgroup that takes its CU's
-  // whole LDS shares no CU -- and no SIMD issue slots -- with a concurrent
-  // batch's blocks; the batch runs on the other CUs.  PBFTV_QC_EXCLUSIVE_CU
-  // (read at every arming): "narrow" (the default) for the 8-wave kernel
-  // only -- 2 CUs of 256 (<1 % of a batch's CUs) for a certificate of up to
-  // 8 signatures that no batch slows -- "1" for the wide kernel too (32
-  // CUs), "0" for neither.
+  // Whole CUs for the armed waves (opt-in, PBFTV_QC_EXCLUSIVE_CU, read at
+  // every arming): an armed workgroup that takes its CU's whole LDS shares no
+  // CU -- and no SIMD issue slots -- with a concurrent batch's blocks.
+  // "narrow": the 8-wave kernel only (2 CUs); "1": the 128-wave kernel too
+  // (32 CUs).  Off by default: with PBFTV_QC_YIELD (the default) no armed
+  // kernel is resident beside a batch, and beside one a whole CU costs the
+  // batch ~3 % (each XCD's share waits for its slowest CU).
   const char* e = getenv("PBFTV_QC_EXCLUSIVE_CU");
   const bool wide = a.relay != nullptr;
-  const bool excl = e ? (e[0] == '1' || (!wide && e[0] == 'n')) : !wide;
+  const bool excl = e && (e[0] == '1' || (!wide && e[0] == 'n'));
   const uint32_t lds = excl ? 160u * 1024u : 0u;
   if (lds) {
     static bool attr = false;  // (per instantiation)

@@ -876,3 +876,37 @@ def test_quiesce_during_rotations(oracle_lib, monkeypatch):
     assert not wrong, wrong[:5]
     assert not slow, slow[:5]
     assert frees[0] > 100 and it > 100, (frees[0], it)
+
+
+def test_caller_sync_memcpy_not_held_by_armed_kernel(oracle_lib, monkeypatch):
+    """A caller's synchronous hipMemcpy (the null stream) on the GPU while the
+    keeper holds an armed kernel: the armed kernels run on the highest-priority
+    streams, which HIP keeps on hardware queues of their own, so the copy does
+    not wait for the resident kernel (on a normal-priority stream it waited the
+    whole budget: tools/queue_share.hip).  5-s budget, so a wait would show."""
+    import ctypes
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", "5000")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=3, per_key=8, seed=85)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        for i in range(0, 9, 3):
+            assert v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]).all()
+        assert v.qc_stamps(0)["armed"]
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), 4096) == 0
+        host = np.zeros(4096, np.uint8)
+        try:
+            for kind in (1, 2):  # hipMemcpyHostToDevice, hipMemcpyDeviceToHost
+                t0 = time.perf_counter()
+                assert hip.hipMemcpy(p if kind == 1 else host.ctypes.data, host.ctypes.data if kind == 1 else p,
+                                     4096, kind) == 0
+                assert time.perf_counter() - t0 < 0.2, kind
+        finally:
+            v.close()  # (the free quiesces the armed kernel first)
+            hip.hipFree(p)
