@@ -540,7 +540,8 @@ hipError_t qc_arm(Device& d) {
   for (hipStream_t& q : d.qstream) {
     if (q) continue;
     int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+    const char* pe = getenv("PBFTV_QC_PRIO");  // (experiments) "0": normal-priority armed streams
+    if ((pe && pe[0] == '0') || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
         hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi) != hipSuccess)
       HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
   }
