@@ -910,3 +910,53 @@ def test_caller_sync_memcpy_not_held_by_armed_kernel(oracle_lib, monkeypatch):
         finally:
             v.close()  # (the free quiesces the armed kernel first)
             hip.hipFree(p)
+
+
+@pytest.mark.parametrize("mode", ["yield", "launched"])
+def test_certificates_beside_a_batch(oracle_lib, mode, monkeypatch):
+    """Certificates while a large batch runs on the context's own stream:
+    "yield" (PBFTV_QC_YIELD=1): the batch enqueue halts the armed kernel, the
+    certificate is launched meanwhile, and the keeper arms again once the batch
+    is expected done; "launched" (PBFTV_QC_ARM=0): every certificate is a
+    launch.  Either way the launch goes to the latency stream, never behind the
+    batch queued on the context stream: it returns long before the batch
+    (several ms of queued work) has finished.  Every bitmap against the oracle."""
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_YIELD" if mode == "yield" else "PBFTV_QC_ARM", "1" if mode == "yield" else "0")
+    monkeypatch.setenv("PBFTV_GBITS", "24")
+    monkeypatch.setenv("PBFTV_QBITS", "16")
+    keys, H, S, K = oracle_sign_pool(oracle_lib, 4, 16, seed=93)
+    S[::5, 9] ^= 0x08
+    n_all = len(K)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(H.ctypes.data, S.ctypes.data, K.ctypes.data, n_all, keys.ctypes.data,
+                                              len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    n = 1 << 20
+    reps = n // n_all
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        dh, ds, dk = (v.to_device(0, np.tile(a, (reps, 1)) if a.ndim > 1 else np.tile(a, reps)) for a in (H, S, K))
+        db = v.alloc(0, n // 8 + 1)
+        try:
+            for i in range(0, 9, 3):  # idle: armed (yield) or launched
+                assert (v.verify_batch(H[i:i + 3], S[i:i + 3], K[i:i + 3]) == want[i:i + 3]).all()
+            for _ in range(6):  # ~6 ms of queued work on the context stream
+                v.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr)
+            t0 = time.perf_counter()
+            got = v.verify_batch(H[9:12], S[9:12], K[9:12])
+            dt = time.perf_counter() - t0
+            assert (got == want[9:12]).all()
+            assert not v.qc_stamps(0)["armed"]  # halted (yield) or never armed
+            assert dt < 3e-3, dt  # not behind the six queued batches
+            v.sync(0)
+            assert (np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool) == np.tile(want, reps)).all()
+            if mode == "yield":
+                time.sleep(0.05)  # past the batches' expected end: the keeper arms again
+                for i in range(12, 30, 3):
+                    assert (v.verify_batch(H[i:i + 3], S[i:i + 3], K[i:i + 3]) == want[i:i + 3]).all()
+                assert v.qc_stamps(0)["armed"]
+        finally:
+            for b in (dh, ds, dk, db):
+                b.free()
