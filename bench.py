@@ -234,7 +234,12 @@ def save_batch(n_global: int, keys: int) -> str:
     ranks through read-only files (tmpfs when there is one): N ranks would
     otherwise each sign the same million messages on the same host cores."""
     import tempfile
-    base = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
+    need = 2 * 110 * n_global + (1 << 20)  # ~101 B per signature (hash, r||s, key, ok) with room to spare
+    base = None
+    if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK):
+        st = os.statvfs("/dev/shm")
+        if st.f_bavail * st.f_frsize >= need:  # (a container's /dev/shm can be as small as 64 MB)
+            base = "/dev/shm"
     dd = tempfile.mkdtemp(prefix="pbftv_bench_", dir=base)
     pub, H, S, K, ok = synth.config4(n_global, n_keys=keys, seed=0x50424654)
     for name, a in (("pub", pub), ("H", H), ("S", S), ("K", K), ("ok", ok)):
