@@ -165,6 +165,7 @@ struct ArmArgs {
   uint64_t* relay;     // wide kernel (kQcCap waves): device word {number, n}, zeroed before launch; null: narrow
   uint32_t stamps;     // 1: each serving wave writes its GPU timestamps (pbftv_qc_stamps*; PBFTV_QC_STAMPS=1)
   int slot;            // its armed stream slot: the expired word and live words it writes (QcMail)
+  uint32_t slots;      // narrow row-schedule kernel: signature slots armed (<= kQcSlots; one workgroup each)
 };
 hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st);
 

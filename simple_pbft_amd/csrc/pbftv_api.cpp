@@ -212,7 +212,9 @@ struct Device {
   int arm_stream = 1;                      // qstream index of the armed kernel
   uint32_t armed_first = 0;                // the armed kernel's first number (its `live` report)
   uint32_t retiring = 0;                   // a rotated-out kernel still waiting for arm_seq's to start
-  uint32_t arm_waves = 0;                  // waves of the armed kernel: kQcSlots (narrow) or kQcCap (wide)
+  uint32_t arm_waves = 0;                  // signatures the armed kernel serves: its slots (narrow) or kQcCap (wide)
+  uint32_t qc_nmax = 0;                    // largest narrow certificate since the last arming
+  uint32_t qc_slots = 4;                   // slots the next narrow arming takes (the row schedule: a CU each)
   std::chrono::steady_clock::time_point last_wide{};  // the last latency-path call of 9..kQcCap signatures
   std::chrono::steady_clock::time_point armed_at{}, last_qc{};
   // diagnostics of the last latency-path call (pbftv_qc_stamps)
@@ -564,12 +566,34 @@ hipError_t qc_arm(Device& d) {
     relay = reinterpret_cast<uint64_t*>(d.qrelay.as<uint8_t>() + 64 * slot);
     HIP_TRY_E(hipMemsetAsync(relay, 0, 8, d.qstream[slot]));  // after that stream's previous kernel left
   }
+  // Narrow slots: the row schedule's armed kernel holds one CU per slot, so it
+  // arms as many as the largest certificate of the last period (kept while no
+  // call came), at least 4 (a 3-vote certificate of a 4-replica committee, the
+  // reference's default, and its 4-vote form); a larger one is served by a
+  // launch and re-arms wider at once.  PBFTV_QC_SLOTS=k fixes k (1..8).
+  if (d.qc_nmax) d.qc_slots = std::max<uint32_t>(4, d.qc_nmax);
+  d.qc_nmax = 0;
+  const char* re = getenv("PBFTV_QC_ROWS");
+  const char* ke = getenv("PBFTV_QC_SLOTS");
+  uint32_t slots = (re && re[0] == '0') ? QcMail::kQcSlots : d.qc_slots;
+  if (ke && atoi(ke) >= 1 && atoi(ke) <= (int)QcMail::kQcSlots) slots = (uint32_t)atoi(ke);
   const char* se = getenv("PBFTV_QC_STAMPS");
-  const ArmArgs a{qc_mail(d), want, qc_arm_budget(d.id), d.key_valid.as<uint32_t>(), d.nkeys, d.gtab->as<uint32_t>(),
-                  d.qptrs.as<const uint32_t* const>(), qc_spin(), halt, relay, se && se[0] == '1' ? 1u : 0u, slot};
+  const ArmArgs a{qc_mail(d),
+                  want,
+                  qc_arm_budget(d.id),
+                  d.key_valid.as<uint32_t>(),
+                  d.nkeys,
+                  d.gtab->as<uint32_t>(),
+                  d.qptrs.as<const uint32_t* const>(),
+                  qc_spin(),
+                  halt,
+                  relay,
+                  se && se[0] == '1' ? 1u : 0u,
+                  slot,
+                  slots};
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = d.armed_first = want;
-  d.arm_waves = relay ? kQcCap : QcMail::kQcSlots;
+  d.arm_waves = relay ? kQcCap : slots;
   d.arm_stream = slot;
   d.armed_at = std::chrono::steady_clock::now();
   if (!d.keeper.joinable() && qc_keep_ms() > 0) d.keeper = std::thread(qc_keeper_loop, &d);
@@ -1804,6 +1828,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     }
     uint32_t cur = 0;  // the armed request number serving this call
     if (n > QcMail::kQcSlots && small) d.last_wide = h_in;
+    if (n <= QcMail::kQcSlots) d.qc_nmax = std::max(d.qc_nmax, (uint32_t)n);
     if (d.arm_seq && n <= d.arm_waves) {
       cur = d.arm_seq;
       if (n > QcMail::kQcSlots) {  // the helpers' inputs (slots kQcSlots..n-1), before any slot tag
@@ -1844,7 +1869,8 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       int rc = launch_plain();
       if (rc != PBFTV_OK) return rc;
       if (small) {
-        if (d.arm_seq && n > d.arm_waves && qc_wide_wanted(d)) HIP_TRY(qc_rotate(d));
+        if (d.arm_seq && n > d.arm_waves && (qc_wide_wanted(d) || n <= QcMail::kQcSlots))
+          HIP_TRY(qc_rotate(d));  // wide, or more narrow slots (qc_nmax), for the next one
         HIP_TRY(qc_arm(d));  // the next call's server (no-op while one is armed)
       }
     }

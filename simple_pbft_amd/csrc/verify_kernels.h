@@ -15,6 +15,7 @@
 
 #include "kernels.h"
 #include "p256_algo.h"
+#include "rows.h"
 
 namespace pbftv {
 
@@ -42,6 +43,24 @@ static __device__ uint64_t g_scal_probe[8192 * 8];
   } while (0)
 #else
 #define PBFTV_SPROBE(k, dep) \
+  do {                       \
+  } while (0)
+#endif
+
+// The row schedule's stage stamps (tools/rows_probe.hip defines
+// PBFTV_ROWS_PROBE before including this header): lane 0 of every wave of the
+// first 128 workgroups, 16 slots per wave.
+#ifdef PBFTV_ROWS_PROBE
+static __device__ uint64_t g_rows_probe[128 * 8 * 16];
+#define PBFTV_RPROBE(k, dep)                                                                  \
+  do {                                                                                        \
+    asm volatile("" ::"v"(dep));                                                              \
+    const uint64_t t_ = wall_clock64();                                                       \
+    if ((threadIdx.x & 63u) == 0 && blockIdx.x < 128)                                         \
+      g_rows_probe[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 16 + (k)] = t_;                    \
+  } while (0)
+#else
+#define PBFTV_RPROBE(k, dep) \
   do {                       \
   } while (0)
 #endif
@@ -1119,37 +1138,236 @@ __device__ __forceinline__ bool wave_verify_words(uint32_t e[8], uint32_t r[8], 
   return ok;
 }
 
+// ---- the row schedule (round 5): EIGHT waves per signature ----------------
+// rows.h holds one field element per VGPR (limb j in lane j of a 16-lane row),
+// so a wave does four products at once and an XYZZ addition costs ~0.95 µs
+// instead of a quad-schedule level's ~2.6 µs.  A workgroup of eight waves
+// verifies one signature:
+//   * wave 0 runs Go's range checks and the scalars (the s^-1 chain, as
+//     wave_verify_words) and hands u1, u2 and r R to the others through LDS;
+//   * wave w takes windows 2w (rows 0, 1) and 2w + 1 (rows 2, 3): the G entry
+//     of digit w of u1 plus the Q entry of digit w of u2 (mmadd_pairs: the
+//     two windows side by side), then their sum (xyzz_add_rows);
+//   * a tree over the waves through LDS: levels 1 and 2 add wave w + m into
+//     wave w; the last (wave 4 into wave 0) is fused with the x check
+//     against r (xyzz_add_check_rows).
+// As in the quad schedule, a doubling or cancellation anywhere leaves a zero
+// ZZ that every later product keeps (one test at the top), a live window with
+// two zero digits and r + n < p (adversarial r only) go to wave 0's exact
+// lane-per-window rerun.  Every thread of the workgroup calls it; the
+// arguments are read from wave 0 only; wave 0 returns the verdict.
+constexpr int kRowWaves = 8;
+#ifndef PBFTV_ROWS_PRIO
+#define PBFTV_ROWS_PRIO 0
+#endif
+
+struct RowsShared {
+  uint32_t ctl;  // bit 0: verify (range checks passed), bit 1: exact path (r + n < p), bit 2: a rare window
+  uint32_t ready[kRowWaves];  // wave w's partial sum is in pts[w]
+  uint32_t u1[8], u2[8], rm[9];
+  uint64_t qtab;
+  uint32_t pts[kRowWaves][4][16];  // a wave's partial sum: row 0's lanes of X, Y, ZZ, ZZZ
+};
+
+template <int WG, int WQ>
+struct RowsGeom {
+  static constexpr int nW = CombGeom<WG>::kWin > CombGeom<WQ>::kWin ? CombGeom<WG>::kWin : CombGeom<WQ>::kWin;
+  static constexpr bool ok = nW > 8 && nW <= 2 * kRowWaves;
+};
+
+// window `win`'s entry of digit d as row-layout x, y (lane L < 9: limb L; the
+// lane reads the two words of each coordinate its limb spans, one 64-B line)
+template <int W>
+__device__ __forceinline__ void row_entry(const uint4* __restrict__ tab, int win, int d, int L, uint32_t& x,
+                                          uint32_t& y) {
+  const int idx = (d < 0 ? -d : d) - 1;
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(tab + (CombGeom<W>::base(win) + (idx < 0 ? 0 : idx)) * 4);
+  const int Lc = L < 9 ? L : 0, bit = 29 * Lc, wi = bit >> 5, sh = bit & 31;
+  const int wj = wi < 7 ? wi + 1 : wi;
+  const uint32_t x0 = p[wi], x1 = p[wj], y0 = p[8 + wi], y1 = p[8 + wj];
+  const uint32_t m = L < 9 ? kMask29 : 0u;
+  x = __builtin_amdgcn_alignbit(wi < 7 ? x1 : 0u, x0, (uint32_t)sh) & m;
+  y = __builtin_amdgcn_alignbit(wi < 7 ? y1 : 0u, y0, (uint32_t)sh) & m;
+}
+
+template <int WG, int WQ>
+__device__ __forceinline__ bool block_verify_rows(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
+                                                  bool key_ok, const uint4* __restrict__ gtab,
+                                                  const uint4* qtab, RowsShared* sh) {
+  constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin, nW = RowsGeom<WG, WQ>::nW;
+  static_assert(RowsGeom<WG, WQ>::ok, "two windows per wave, eight waves");
+  const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
+  PBFTV_RPROBE(0, e[0]);
+  if (wv == 0) {
+    uint32_t ctl = 0;
+    if (key_ok && !words_is_zero(r) && !words_is_zero(s) && words_lt(r, kN32) && words_lt(s, kN32)) {
+      uint32_t u1[8], u2[8];
+      fe rm, rnm;
+      bool rn_ok;
+      wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
+      ctl = rn_ok ? 3u : 1u;
+      uint32_t a = 0, b = 0;
+      PBFTV_UNROLL for (int k = 0; k < 8; ++k) {
+        a = lane == k ? u1[k] : a;
+        b = lane == k ? u2[k] : b;
+      }
+      if (lane < 8) {
+        sh->u1[lane] = a;
+        sh->u2[lane] = b;
+      }
+      if (lane < 9) sh->rm[lane] = limb_of(rm.v, lane);
+      if (lane == 0) sh->qtab = (uint64_t)(uintptr_t)qtab;
+    }
+    if (lane == 0) sh->ctl = ctl;
+    if (lane < kRowWaves) sh->ready[lane] = 0u;
+    PBFTV_RPROBE(1, ctl);
+  }
+  __syncthreads();
+  const uint32_t ctl = (uint32_t)__builtin_amdgcn_readfirstlane((int)sh->ctl);
+  if (!(ctl & 1u)) return false;  // (every wave: the same LDS word)
+  uint32_t u1[8], u2[8];
+  PBFTV_UNROLL for (int k = 0; k < 8; ++k) {
+    u1[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sh->u1[k]);
+    u2[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sh->u2[k]);
+  }
+  const uint64_t qv = sh->qtab;
+  const uint4* qt = reinterpret_cast<const uint4*>(
+      (uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(qv >> 32)) << 32) |
+                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)qv)));
+  if (ctl & 2u) {  // r + n < p: the exact path, wave 0 alone (no barrier follows)
+    if (wv != 0) return false;
+    jac P;
+    bool inf;
+    wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qt);
+    return ecdsa_check(P, !inf, r);
+  }
+  if (2 * wv >= nW) return false;  // no window (its partners know that statically)
+#if PBFTV_ROWS_PRIO == 1  // (experiments) the right subtree (waves 4..7, each the younger wave of its SIMD) first
+  if (wv >= kRowWaves / 2) __builtin_amdgcn_s_setprio(3); else __builtin_amdgcn_s_setprio(2);
+#endif
+  const RowCtx c = row_ctx();
+  const uint32_t rml = c.L < 9 ? sh->rm[c.L] : 0u;
+  PBFTV_RPROBE(2, rml);
+  // digits of every window (quad q = window q), each row pair keeps its own
+  const int q = lane >> 2;
+  const int d1 = lane_window_digit<WG>(u1, q), d2 = lane_window_digit<WQ>(u2, q);
+  const int wA = 2 * wv, wB = 2 * wv + 1;
+  const int a1 = __builtin_amdgcn_readlane(d1, 4 * wA), a2 = __builtin_amdgcn_readlane(d2, 4 * wA);
+  const int b1 = __builtin_amdgcn_readlane(d1, 4 * wB), b2 = __builtin_amdgcn_readlane(d2, 4 * wB);
+  const bool pb = c.row >= 2;
+  const int win = pb ? wB : wA, g1 = pb ? b1 : a1, g2 = pb ? b2 : a2;
+  uint32_t gx, gy, qx, qy;
+  row_entry<WG>(gtab, win < nG ? win : 0, g1, c.L, gx, gy);
+  row_entry<WQ>(qt, win < nQ ? win : 0, g2, c.L, qx, qy);
+  gy = g1 < 0 ? 0u - gy : gy;
+  qy = g2 < 0 ? 0u - qy : qy;
+  PBFTV_RPROBE(3, gx ^ gy ^ qx ^ qy);
+  xyzz_r S;
+  mmadd_pairs(c, S, gx, gy, qx, qy);  // (x-coordinates meeting: PP = 0 = ZZ, tested at the top)
+  const bool both = g1 != 0 && g2 != 0, gonly = g1 != 0;
+  PBFTV_RPROBE(4, S.y);
+  xyzz_r Pw;  // a lone table point: ZZ = ZZZ = 1
+  Pw.x = both ? S.x : (gonly ? gx : qx);
+  Pw.y = both ? S.y : (gonly ? gy : qy);
+  Pw.zz = both ? S.zz : c.one;
+  Pw.zzz = both ? S.zzz : c.one;
+  // a live window with two zero digits (probability ~2^-50): the exact rerun
+  if (__any(win < nW && g1 == 0 && g2 == 0) && lane == 0) atomicOr(&sh->ctl, 4u);
+  xyzz_r P, B;
+  uint32_t rz = 0, g[4];
+  gather4(g, Pw.x);
+  P.x = g[0];
+  B.x = g[2];
+  gather4(g, Pw.y);
+  P.y = g[0];
+  B.y = g[2];
+  gather4(g, Pw.zz);
+  P.zz = g[0];
+  B.zz = g[2];
+  gather4(g, Pw.zzz);
+  P.zzz = g[0];
+  B.zzz = g[2];
+  if (wB < nW) xyzz_add_rows(c, P, rz, P, B, rml);
+  PBFTV_RPROBE(5, P.y);
+  // The tree: at level m a wave w with w mod 2m == m hands its sum to wave
+  // w - m and leaves; the holder waits for that one partner only (an LDS flag,
+  // release / acquire at workgroup scope), not for the whole workgroup, so a
+  // wave whose subtree is ready early goes on while slower ones still add.
+  bool ok = false, exc = false;
+  PBFTV_UNROLL for (int m = 1; m < kRowWaves; m <<= 1) {
+    if ((wv & (2 * m - 1)) == m) {
+      if (c.row == 0) {
+        sh->pts[wv][0][c.L] = P.x;
+        sh->pts[wv][1][c.L] = P.y;
+        sh->pts[wv][2][c.L] = P.zz;
+        sh->pts[wv][3][c.L] = P.zzz;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&sh->ready[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    if (2 * (wv + m) < nW) {  // add the partner's
+      while (__hip_atomic_load(&sh->ready[wv + m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      PBFTV_RPROBE(5 + 2 * m - (m == 4 ? 1 : 0), m);
+      xyzz_r Q;
+      Q.x = sh->pts[wv + m][0][c.L];
+      Q.y = sh->pts[wv + m][1][c.L];
+      Q.zz = sh->pts[wv + m][2][c.L];
+      Q.zzz = sh->pts[wv + m][3][c.L];
+      if (m == kRowWaves / 2) {  // wave 0: the last level, fused with the check
+        ok = xyzz_add_check_rows(c, exc, P, Q, rz);
+      } else {
+        xyzz_add_rows(c, P, rz, P, Q, rml);
+      }
+    }
+    PBFTV_RPROBE(6 + 2 * m - (m == 4 ? 1 : 0), P.y ^ (uint32_t)ok);
+  }
+  if (wv != 0) return false;
+  exc = exc || (sh->ctl & 4u) != 0;
+  if (exc) {  // a doubling / cancellation somewhere, or a rare window: exact rerun
+    jac R;
+    bool inf;
+    wave_sum_lanes<WG, WQ>(R, inf, u1, u2, gtab, qt);
+    ok = ecdsa_check(R, !inf, r);
+  }
+  return ok;
+}
+
 // ... from memory: signature i of the (host or device) input arrays.
+__device__ __forceinline__ void wave_load_sig(const uint8_t* __restrict__ hashes, const uint8_t* __restrict__ sigs,
+                                              const uint32_t* __restrict__ key_idx, uint64_t i,
+                                              const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                              const uint4* const* __restrict__ qtabs, uint32_t e[8], uint32_t r[8],
+                                              uint32_t s[8], bool& key_ok, const uint4*& qtab) {
+  load_be256(hashes + 32 * i, e);  // one round trip to the (host) inputs
+  load_be256(sigs + 64 * i, r);
+  load_be256(sigs + 64 * i + 32, s);
+  const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)key_idx[i]);
+  key_ok = k < nkeys && key_valid[k] != 0;
+  qtab = qtabs[k < nkeys ? k : 0];  // (loaded now: ready when the scalars are)
+  PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // one copy per wave (the loads are per lane)
+    e[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[t]);
+    r[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[t]);
+    s[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[t]);
+  }
+}
+
 template <int WG, int WQ>
 __device__ __forceinline__ bool wave_verify_sig(const uint8_t* __restrict__ hashes, const uint8_t* __restrict__ sigs,
                                                 const uint32_t* __restrict__ key_idx, uint64_t i,
                                                 const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                 const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs) {
   uint32_t r[8], s[8], e[8];
-  load_be256(hashes + 32 * i, e);  // one round trip to the (host) inputs
-  load_be256(sigs + 64 * i, r);
-  load_be256(sigs + 64 * i + 32, s);
-  const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)key_idx[i]);
-  const bool key_ok = k < nkeys && key_valid[k] != 0;
-  const uint4* qtab = qtabs[k < nkeys ? k : 0];  // (loaded now: ready when the scalars are)
-  PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // one copy per wave (the loads are per lane)
-    e[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[t]);
-    r[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)r[t]);
-    s[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[t]);
-  }
+  bool key_ok;
+  const uint4* qtab;
+  wave_load_sig(hashes, sigs, key_idx, i, key_valid, nkeys, qtabs, e, r, s, key_ok, qtab);
   return wave_verify_words<WG, WQ>(e, r, s, key_ok, gtab, qtab);
 }
 
-template <int WG, int WQ>
-__global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ hashes,
-                                                   const uint8_t* __restrict__ sigs,
-                                                   const uint32_t* __restrict__ key_idx, uint64_t n,
-                                                   const uint32_t* __restrict__ key_valid, uint32_t nkeys,
-                                                   const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
-                                                   uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
-  const uint64_t i = blockIdx.x;
-  const bool ok = wave_verify_sig<WG, WQ>(hashes, sigs, key_idx, i, key_valid, nkeys, gtab, qtabs);
-  if (threadIdx.x != 0) return;
+__device__ __forceinline__ void wave_store_verdict(bool ok, uint64_t i, uint64_t n, uint8_t* __restrict__ bitmap,
+                                                   uint8_t* __restrict__ okbytes) {
   if (okbytes) {
     okbytes[i] = ok ? 1 : 0;
     return;
@@ -1167,6 +1385,37 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
   if (i + 1 == n) clear |= ((0xFEu << (unsigned)(i & 7)) & 0xFFu) << sh;
   if (clear) atomicAnd(word, ~clear);
   if (ok) atomicOr(word, bit);
+}
+
+template <int WG, int WQ>
+__global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ hashes,
+                                                   const uint8_t* __restrict__ sigs,
+                                                   const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                   const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                                   const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
+                                                   uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+  const uint64_t i = blockIdx.x;
+  const bool ok = wave_verify_sig<WG, WQ>(hashes, sigs, key_idx, i, key_valid, nkeys, gtab, qtabs);
+  if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
+}
+
+// the row schedule, launched: one 512-thread workgroup per signature
+template <int WG, int WQ>
+__global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows(const uint8_t* __restrict__ hashes,
+                                                               const uint8_t* __restrict__ sigs,
+                                                               const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                               const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                                               const uint4* __restrict__ gtab,
+                                                               const uint4* const* __restrict__ qtabs,
+                                                               uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+  __shared__ RowsShared sh;
+  const uint64_t i = blockIdx.x;
+  uint32_t e[8] = {}, r[8] = {}, s[8] = {};
+  bool key_ok = false;
+  const uint4* qtab = nullptr;
+  if (threadIdx.x < 64) wave_load_sig(hashes, sigs, key_idx, i, key_valid, nkeys, qtabs, e, r, s, key_ok, qtab);
+  const bool ok = block_verify_rows<WG, WQ>(e, r, s, key_ok, gtab, qtab, &sh);
+  if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
 }
 
 // ---- the armed latency kernel ------------------------------------------------
@@ -1354,6 +1603,116 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
   }
 }
 
+// The narrow armed server on the row schedule: one 512-thread workgroup per
+// slot.  Wave 0 is the slot wave of k_ecdsa_wave_armed (the same polls,
+// exits, live / expired words and verdict store); the other seven wait at the
+// workgroup barrier -- they issue nothing while they wait -- and join
+// block_verify_rows when wave 0 has a signature for the slot.
+template <int WG, int WQ>
+__global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) {
+  __shared__ RowsShared sh;
+  __shared__ uint32_t cmd;  // 0: leave, 1: serve the slot, 2: request without this slot
+  const uint32_t b = blockIdx.x, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  QcMail* const mail = a.mail;
+  uint8_t* const base = reinterpret_cast<uint8_t*>(mail);
+  uint32_t want = a.want;
+  const uint64_t t0 = wall_clock64();
+  if (wv == 0 && lane == 0) reinterpret_cast<volatile uint32_t*>(base + QcMail::live_off(a.slot))[b] = want;
+  const uint32_t nkeys = a.nkeys;
+  const uint4* qt_lo = nullptr;
+  const uint4* qt_hi = nullptr;
+  uint32_t kv_lo = 0, kv_hi = 0;
+  if (wv == 0) {  // key data for keys < 128, two per lane
+    qt_lo = lane < nkeys ? reinterpret_cast<const uint4* const*>(a.qtabs)[lane] : nullptr;
+    qt_hi = lane + 64 < nkeys ? reinterpret_cast<const uint4* const*>(a.qtabs)[lane + 64] : nullptr;
+    kv_lo = lane < nkeys ? a.key_valid[lane] : 0u;
+    kv_hi = lane + 64 < nkeys ? a.key_valid[lane + 64] : 0u;
+  }
+  const uint4* gtab = reinterpret_cast<const uint4*>(a.gtab);
+  const uint4* const* qtabs = reinterpret_cast<const uint4* const*>(a.qtabs);
+  const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b));
+  const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
+  for (;; ++want) {
+    uint32_t e[8] = {}, r[8] = {}, s[8] = {};
+    bool key_ok = false;
+    const uint4* qtab = nullptr;
+    uint64_t seen_wall = 0, seen_clk = 0;
+    if (wv == 0) {
+      uint32_t v = 0;
+      bool serve = false;
+      for (;;) {
+        v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (__builtin_amdgcn_readlane(v, 0) == want && __builtin_amdgcn_readlane(v, 15) == want &&
+            (b >= __builtin_amdgcn_readlane(v, 1) ||
+             (__builtin_amdgcn_readlane(v, 16) == want && __builtin_amdgcn_readlane(v, 31) == want &&
+              __builtin_amdgcn_readlane(v, 32) == want && __builtin_amdgcn_readlane(v, 47) == want))) {
+          serve = true;
+          break;
+        }
+        if (__builtin_amdgcn_readlane(v, 48 + 2) == want || __builtin_amdgcn_readlane(v, 48 + 5) != a.halt ||
+            wall_clock64() - t0 > a.budget)
+          break;  // header stop / halt, or the budget
+        if (a.spin == 0) {
+          __builtin_amdgcn_s_sleep(2);
+        } else if (a.spin >= 1000) {  // (experiments) (spin - 1000) x s_sleep(8) between polls
+          for (uint32_t j = 1000; j < a.spin; ++j) __builtin_amdgcn_s_sleep(8);
+        } else if (a.spin > 1) {
+          uint32_t x = lane;
+          for (uint32_t j = 0; j < a.spin; ++j) asm volatile("v_mad_u32_u24 %0, %0, %0, %0" : "+v"(x));
+        }
+      }
+      uint32_t c = 0;
+      if (!serve) {
+        if (lane == 0) __hip_atomic_store(mail->expired(a.slot), want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        seen_wall = wall_clock64();
+        seen_clk = clock64();
+        const uint32_t n = __builtin_amdgcn_readlane(v, 1);
+        c = b < n ? 1u : 2u;
+        if (c == 1u) {
+          const uint32_t k = __builtin_amdgcn_readlane(v, 2);
+          PBFTV_UNROLL for (int t = 0; t < 8; ++t) {  // slot line j, dword 4 + t = LE dword t of the hash / r / s
+            e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 4 + t));
+            r[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 20 + t));
+            s[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 36 + t));
+          }
+          armed_key(k, nkeys, qt_lo, qt_hi, kv_lo, kv_hi, a.key_valid, qtabs, key_ok, qtab);
+        }
+      }
+      if (lane == 0) cmd = c;
+    }
+    __syncthreads();
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)cmd);
+    __syncthreads();  // (cmd is rewritten only after every wave has read it)
+    if (c == 0u) return;
+    if (c == 2u) continue;
+    __builtin_amdgcn_s_setprio(3);
+    const bool ok = block_verify_rows<WG, WQ>(e, r, s, key_ok, gtab, qtab, &sh);
+    if (wv == 0 && lane == 0) {
+      constexpr uint32_t cap = QcMail::kQcCap;
+      if (a.stamps) {
+        volatile uint64_t* st = reinterpret_cast<volatile uint64_t*>(base + QcMail::stamps_off(cap)) + 4 * b;
+        st[0] = seen_wall;  // diagnostics (pbftv_qc_stamps), before the verdict
+        st[1] = seen_clk;
+        st[2] = wall_clock64();
+        st[3] = clock64();
+      }
+      reinterpret_cast<volatile uint8_t*>(base)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+// the row schedule (PBFTV_QC_ROWS=0: the quad schedule, for A/B), read at every launch
+inline bool rows_enabled() {
+  const char* e = getenv("PBFTV_QC_ROWS");
+  return !(e && e[0] == '0');
+}
+inline uint64_t rows_max_batch() {  // launched: the row schedule up to this many signatures
+  const char* e = getenv("PBFTV_QC_ROWS_MAX");
+  return e ? strtoull(e, nullptr, 10) : 128;
+}
+
 template <int WG, int WQ>
 void launch_armed_w(const ArmArgs& a, hipStream_t st) {
   // Whole CUs for the armed waves (opt-in, PBFTV_QC_EXCLUSIVE_CU, read at
@@ -1366,6 +1725,22 @@ void launch_armed_w(const ArmArgs& a, hipStream_t st) {
   const char* e = getenv("PBFTV_QC_EXCLUSIVE_CU");
   const bool wide = a.relay != nullptr;
   const bool excl = e && (e[0] == '1' || (!wide && e[0] == 'n'));
+  if constexpr (RowsGeom<WG, WQ>::ok) {
+    if (!wide && rows_enabled()) {
+      const uint32_t rl = excl ? 160u * 1024u - 4096u : 0u;  // (+ the kernel's static LDS)
+      if (rl) {
+        static bool rattr = false;
+        if (!rattr) {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ecdsa_rows_armed<WG, WQ>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)rl);
+          rattr = true;
+        }
+      }
+      const uint32_t slots = a.slots >= 1 && a.slots <= QcMail::kQcSlots ? a.slots : QcMail::kQcSlots;
+      hipLaunchKernelGGL((k_ecdsa_rows_armed<WG, WQ>), dim3(slots), dim3(64 * kRowWaves), rl, st, a);
+      return;
+    }
+  }
   const uint32_t lds = excl ? 160u * 1024u : 0u;
   if (lds) {
     static bool attr = false;  // (per instantiation)
@@ -1384,6 +1759,14 @@ void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* k
                           const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
                           const uint32_t* const* qtabs,
                           uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
+  if constexpr (RowsGeom<WG, WQ>::ok) {
+    if (n <= rows_max_batch() && rows_enabled()) {
+      hipLaunchKernelGGL((k_ecdsa_rows<WG, WQ>), dim3((uint32_t)n), dim3(64 * kRowWaves), 0, st, hashes, sigs, key_idx,
+                         n, key_valid, nkeys, reinterpret_cast<const uint4*>(gtab),
+                         reinterpret_cast<const uint4* const*>(qtabs), bitmap, okbytes);
+      return;
+    }
+  }
   hipLaunchKernelGGL((k_ecdsa_wave<WG, WQ>), dim3((uint32_t)n), dim3(64), 0, st, hashes, sigs, key_idx, n, key_valid,
                      nkeys, reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4* const*>(qtabs), bitmap,
                      okbytes);

@@ -1,0 +1,135 @@
+// rows_probe.hip -- stage stamps of the row schedule (k_ecdsa_rows, the
+// launched latency kernel: eight waves per signature, verify_kernels.h
+// block_verify_rows), built with PBFTV_ROWS_PROBE: wall_clock64() of wave 0
+// at each stage boundary.  Tables: the n = 4 geometry (29-bit G, one 24-bit
+// key table with Q = G), built with the product's table kernels.  Measurement
+// tool for DESIGN.md (not the product).
+//   make -C simple_pbft_amd && hipcc --offload-arch=gfx950 -O3 -std=c++17 -c tools/rows_probe.hip -o /tmp/rp.o \
+//   && hipcc --offload-arch=gfx950 /tmp/rp.o simple_pbft_amd/build/p256_*.o -o tools/rows_probe
+#define PBFTV_ROWS_PROBE 1
+#include "../simple_pbft_amd/csrc/verify_kernels.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+using namespace pbftv;
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+constexpr int WG = 29, WQ = 24;
+
+// k_ecdsa_rows' body in a kernel of this unit (the library's objects carry
+// their own, unstamped, instantiation of the template)
+__global__ void __launch_bounds__(64 * kRowWaves) rows_probe_k(const uint8_t* __restrict__ hashes,
+                                                               const uint8_t* __restrict__ sigs,
+                                                               const uint32_t* __restrict__ key_idx, uint64_t n,
+                                                               const uint32_t* __restrict__ key_valid, uint32_t nkeys,
+                                                               const uint4* __restrict__ gtab,
+                                                               const uint4* const* __restrict__ qtabs,
+                                                               uint8_t* __restrict__ bitmap) {
+  __shared__ RowsShared sh;
+  const uint64_t i = blockIdx.x;
+  uint32_t e[8] = {}, r[8] = {}, s[8] = {};
+  bool key_ok = false;
+  const uint4* qtab = nullptr;
+  if (threadIdx.x < 64) wave_load_sig(hashes, sigs, key_idx, i, key_valid, nkeys, qtabs, e, r, s, key_ok, qtab);
+  const bool ok = block_verify_rows<WG, WQ>(e, r, s, key_ok, gtab, qtab, &sh);
+  if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, nullptr);
+}
+
+int main() {
+  const uint32_t n = 64;
+  // key = G (valid), random in-range r, s, e: the stages run in full whatever the verdict
+  std::vector<uint8_t> h(32 * n), sg(64 * n), key(64);
+  uint32_t x = 12345;
+  auto rnd = [&]() { x = x * 1664525u + 1013904223u; return (uint8_t)(x >> 24); };
+  for (auto& b : h) b = rnd();
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 64; ++k) sg[64 * i + k] = (k % 32 == 0) ? 0x7F : rnd();  // r, s < n
+  const uint32_t gx[8] = {0xd898c296, 0xf4a13945, 0x2deb33a0, 0x77037d81, 0x63a440f2, 0xf8bce6e5, 0xe12c4247, 0x6b17d1f2};
+  const uint32_t gy[8] = {0x37bf51f5, 0xcbb64068, 0x6b315ece, 0x2bce3357, 0x7c0f9e16, 0x8ee7eb4a, 0xfe1a7f9b, 0x4fe342e2};
+  std::vector<uint32_t> keys_le(16);
+  for (int k = 0; k < 8; ++k) { keys_le[k] = gx[k]; keys_le[8 + k] = gy[k]; }
+  uint8_t *dh, *ds;
+  uint32_t *dk, *dkeys, *dvalid, *dsink;
+  uint64_t* dst;
+  CHECK(hipMalloc(&dh, h.size()));
+  CHECK(hipMalloc(&ds, sg.size()));
+  CHECK(hipMalloc(&dk, 4 * n));
+  CHECK(hipMalloc(&dkeys, 64));
+  CHECK(hipMalloc(&dvalid, 64));
+  CHECK(hipMalloc(&dsink, 4 * n));
+  CHECK(hipMalloc(&dst, 8 * 5 * n));
+  CHECK(hipMemcpy(dh, h.data(), h.size(), hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(ds, sg.data(), sg.size(), hipMemcpyHostToDevice));
+  CHECK(hipMemset(dk, 0, 4 * n));
+  CHECK(hipMemcpy(dkeys, keys_le.data(), 64, hipMemcpyHostToDevice));
+  uint32_t *gt, *qt;
+  CHECK(hipMalloc(&gt, table_bytes(WG)));
+  CHECK(hipMalloc(&qt, table_bytes(WQ)));
+  for (int w : {WG, WQ}) {
+    const TableScratchSizes z = table_scratch_sizes(w, 1);
+    void *b, *l, *hb, *ss, *es;
+    CHECK(hipMalloc(&b, z.bases)); CHECK(hipMalloc(&l, z.lbuf)); CHECK(hipMalloc(&hb, z.hbuf));
+    CHECK(hipMalloc(&ss, z.small_scratch)); CHECK(hipMalloc(&es, z.entry_scratch));
+    TableScratch sc{b, l, hb, ss, es, z.entry_lanes};
+    uint32_t** dtab;
+    uint32_t* tab = w == WG ? gt : qt;
+    CHECK(hipMalloc(&dtab, sizeof(void*)));
+    CHECK(hipMemcpy(dtab, &tab, sizeof(void*), hipMemcpyHostToDevice));
+    CHECK(launch_build_tables(w, dkeys, 0, 1, w == WG ? 1 : 0, dvalid, dtab, sc, 0));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipFree(b)); CHECK(hipFree(l)); CHECK(hipFree(hb)); CHECK(hipFree(ss)); CHECK(hipFree(es));
+  }
+  int rate_khz = 0;
+  CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
+  const uint32_t** dq;
+  CHECK(hipMalloc(&dq, sizeof(void*)));
+  CHECK(hipMemcpy(dq, &qt, sizeof(void*), hipMemcpyHostToDevice));
+  uint8_t* dbm;
+  CHECK(hipMalloc(&dbm, n / 8 + 8));
+  const int kS = 16;
+  const int stages[] = {1, 2, 3, 4, 5, 7, 8, 9, 10, 12, 13};
+  const char* names[] = {"scalars", "handoff", "digits_entries", "level0_mmadd", "wave_pair_add", "l1_barrier",
+                         "l1_add", "l2_barrier", "l2_add", "l3_barrier", "l3_check"};
+  printf("{\"geometry\": [%d, %d]", WG, WQ);
+  for (uint32_t nb : {1u, 3u, 64u}) {
+    for (int rep = 0; rep < 4; ++rep) {
+      hipLaunchKernelGGL(rows_probe_k, dim3(nb), dim3(64 * kRowWaves), 0, 0, dh, ds, dk, (uint64_t)nb, dvalid, 1u,
+                         reinterpret_cast<const uint4*>(gt), reinterpret_cast<const uint4* const*>(dq), dbm);
+      CHECK(hipDeviceSynchronize());
+    }
+    std::vector<uint64_t> st(128 * 8 * kS);
+    CHECK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_rows_probe), 8 * 128 * 8 * kS));
+    printf(", \"n%u\": {", nb);
+    // wave 0's timeline: median over the workgroups of each stage
+    for (size_t k = 0; k < sizeof(stages) / sizeof(int); ++k) {
+      std::vector<double> d;
+      for (uint32_t b = 0; b < nb && b < 128; ++b) {
+        const uint64_t* s = &st[b * 8 * kS];
+        const uint64_t pv = k == 0 ? s[0] : s[stages[k - 1]];
+        d.push_back((double)(s[stages[k]] - pv) * 1e3 / rate_khz);
+      }
+      std::sort(d.begin(), d.end());
+      printf("%s\"%s_us\": %.2f", k ? ", " : "", names[k], d[d.size() / 2]);
+    }
+    std::vector<double> tot;
+    for (uint32_t b = 0; b < nb && b < 128; ++b) tot.push_back((double)(st[b * 8 * kS + 13] - st[b * 8 * kS]) * 1e3 / rate_khz);
+    std::sort(tot.begin(), tot.end());
+    printf(", \"total_us\": %.2f", tot[tot.size() / 2]);
+    // workgroup 0, every wave: handoff end (2) -> entries (3) -> level 0 (4) -> pair add (5), from wave 0's stamp 2
+    printf(", \"wg0_waves_us_since_handoff\": [");
+    for (int w = 0; w < 8; ++w) {
+      const uint64_t* s = &st[w * kS];
+      const uint64_t t2 = st[2];
+      printf("%s[%.2f, %.2f, %.2f, %.2f]", w ? ", " : "", (double)(s[2] - t2) * 1e3 / rate_khz,
+             (double)(s[3] - t2) * 1e3 / rate_khz, (double)(s[4] - t2) * 1e3 / rate_khz, (double)(s[5] - t2) * 1e3 / rate_khz);
+    }
+    printf("]}");
+
+  }
+  printf("}\n");
+  return 0;
+}
