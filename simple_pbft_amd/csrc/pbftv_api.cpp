@@ -1925,6 +1925,22 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         return fail(PBFTV_EDEVICE, "wave verify kernel did not report every signature");
       }
     }
+    if (cur) {
+      // the armed row schedule leaves an exceptional signature (a doubling or
+      // cancellation in its tree, a window with two zero digits, r + n < p) to
+      // the launched kernel's exact path: result byte 2 (rare; adversarial
+      // inputs only)
+      bool rerun = false;
+      for (uint64_t i = 0; i < n; ++i) rerun |= res[i] == 2;
+      if (rerun) {
+        std::memset(const_cast<uint8_t*>(res), 0xFF, n);
+        int rc = launch_plain();
+        if (rc != PBFTV_OK) return rc;
+        HIP_TRY(hipStreamSynchronize(d.lstream));
+        for (uint64_t i = 0; i < n; ++i)
+          if (res[i] == 0xFF) return fail(PBFTV_EDEVICE, "wave verify kernel did not report every signature");
+      }
+    }
     if (d.keeper_idle || (d.arm_seq == 0 && d.keeper.joinable())) {
       // past its keep window, or nothing armed after a larger call: the
       // keeper arms one again as soon as this call releases the device

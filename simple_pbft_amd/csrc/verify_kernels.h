@@ -1157,9 +1157,6 @@ __device__ __forceinline__ bool wave_verify_words(uint32_t e[8], uint32_t r[8], 
 // lane-per-window rerun.  Every thread of the workgroup calls it; the
 // arguments are read from wave 0 only; wave 0 returns the verdict.
 constexpr int kRowWaves = 8;
-#ifndef PBFTV_ROWS_PRIO
-#define PBFTV_ROWS_PRIO 0
-#endif
 
 struct RowsShared {
   uint32_t ctl;  // bit 0: verify (range checks passed), bit 1: exact path (r + n < p), bit 2: a rare window
@@ -1173,6 +1170,7 @@ template <int WG, int WQ>
 struct RowsGeom {
   static constexpr int nW = CombGeom<WG>::kWin > CombGeom<WQ>::kWin ? CombGeom<WG>::kWin : CombGeom<WQ>::kWin;
   static constexpr bool ok = nW > 8 && nW <= 2 * kRowWaves;
+  static constexpr int waves = (nW + 1) / 2;  // launched: waves past the windows would have nothing to do
 };
 
 // window `win`'s entry of digit d as row-layout x, y (lane L < 9: limb L; the
@@ -1190,10 +1188,14 @@ __device__ __forceinline__ void row_entry(const uint4* __restrict__ tab, int win
   y = __builtin_amdgcn_alignbit(wi < 7 ? y1 : 0u, y0, (uint32_t)sh) & m;
 }
 
-template <int WG, int WQ>
-__device__ __forceinline__ bool block_verify_rows(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
-                                                  bool key_ok, const uint4* __restrict__ gtab,
-                                                  const uint4* qtab, RowsShared* sh) {
+// kExact: the exceptional cases run wave 0's exact rerun here (the launched
+// kernel); without it (the armed kernel, which then needs far fewer registers
+// while it stays resident) they return 2 and the host serves the certificate
+// with the launched kernel.  Returns 1 / 0 (valid / not), or 2.
+template <int WG, int WQ, bool kExact>
+__device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
+                                                 bool key_ok, const uint4* __restrict__ gtab,
+                                                 const uint4* qtab, RowsShared* sh) {
   constexpr int nG = CombGeom<WG>::kWin, nQ = CombGeom<WQ>::kWin, nW = RowsGeom<WG, WQ>::nW;
   static_assert(RowsGeom<WG, WQ>::ok, "two windows per wave, eight waves");
   const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
@@ -1224,7 +1226,7 @@ __device__ __forceinline__ bool block_verify_rows(const uint32_t e[8], const uin
   }
   __syncthreads();
   const uint32_t ctl = (uint32_t)__builtin_amdgcn_readfirstlane((int)sh->ctl);
-  if (!(ctl & 1u)) return false;  // (every wave: the same LDS word)
+  if (!(ctl & 1u)) return 0;  // (every wave: the same LDS word)
   uint32_t u1[8], u2[8];
   PBFTV_UNROLL for (int k = 0; k < 8; ++k) {
     u1[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)sh->u1[k]);
@@ -1235,16 +1237,17 @@ __device__ __forceinline__ bool block_verify_rows(const uint32_t e[8], const uin
       (uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(qv >> 32)) << 32) |
                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)qv)));
   if (ctl & 2u) {  // r + n < p: the exact path, wave 0 alone (no barrier follows)
-    if (wv != 0) return false;
-    jac P;
-    bool inf;
-    wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qt);
-    return ecdsa_check(P, !inf, r);
+    if (wv != 0) return 0;
+    if constexpr (kExact) {
+      jac P;
+      bool inf;
+      wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qt);
+      return ecdsa_check(P, !inf, r) ? 1 : 0;
+    } else {
+      return 2;
+    }
   }
-  if (2 * wv >= nW) return false;  // no window (its partners know that statically)
-#if PBFTV_ROWS_PRIO == 1  // (experiments) the right subtree (waves 4..7, each the younger wave of its SIMD) first
-  if (wv >= kRowWaves / 2) __builtin_amdgcn_s_setprio(3); else __builtin_amdgcn_s_setprio(2);
-#endif
+  if (2 * wv >= nW) return 0;  // no window (its partners know that statically)
   const RowCtx c = row_ctx();
   const uint32_t rml = c.L < 9 ? sh->rm[c.L] : 0u;
   PBFTV_RPROBE(2, rml);
@@ -1304,7 +1307,7 @@ __device__ __forceinline__ bool block_verify_rows(const uint32_t e[8], const uin
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sh->ready[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return false;
+      return 0;
     }
     if (2 * (wv + m) < nW) {  // add the partner's
       while (__hip_atomic_load(&sh->ready[wv + m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
@@ -1324,15 +1327,19 @@ __device__ __forceinline__ bool block_verify_rows(const uint32_t e[8], const uin
     }
     PBFTV_RPROBE(6 + 2 * m - (m == 4 ? 1 : 0), P.y ^ (uint32_t)ok);
   }
-  if (wv != 0) return false;
+  if (wv != 0) return 0;
   exc = exc || (sh->ctl & 4u) != 0;
   if (exc) {  // a doubling / cancellation somewhere, or a rare window: exact rerun
-    jac R;
-    bool inf;
-    wave_sum_lanes<WG, WQ>(R, inf, u1, u2, gtab, qt);
-    ok = ecdsa_check(R, !inf, r);
+    if constexpr (kExact) {
+      jac R;
+      bool inf;
+      wave_sum_lanes<WG, WQ>(R, inf, u1, u2, gtab, qt);
+      ok = ecdsa_check(R, !inf, r);
+    } else {
+      return 2;
+    }
   }
-  return ok;
+  return ok ? 1 : 0;
 }
 
 // ... from memory: signature i of the (host or device) input arrays.
@@ -1414,7 +1421,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows(const uint8_t* __
   bool key_ok = false;
   const uint4* qtab = nullptr;
   if (threadIdx.x < 64) wave_load_sig(hashes, sigs, key_idx, i, key_valid, nkeys, qtabs, e, r, s, key_ok, qtab);
-  const bool ok = block_verify_rows<WG, WQ>(e, r, s, key_ok, gtab, qtab, &sh);
+  const bool ok = block_verify_rows<WG, WQ, true>(e, r, s, key_ok, gtab, qtab, &sh) == 1;
   if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
 }
 
@@ -1687,7 +1694,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
     if (c == 0u) return;
     if (c == 2u) continue;
     __builtin_amdgcn_s_setprio(3);
-    const bool ok = block_verify_rows<WG, WQ>(e, r, s, key_ok, gtab, qtab, &sh);
+    const int ok = block_verify_rows<WG, WQ, false>(e, r, s, key_ok, gtab, qtab, &sh);  // 2: the host reruns it
     if (wv == 0 && lane == 0) {
       constexpr uint32_t cap = QcMail::kQcCap;
       if (a.stamps) {
@@ -1697,7 +1704,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
         st[2] = wall_clock64();
         st[3] = clock64();
       }
-      reinterpret_cast<volatile uint8_t*>(base)[QcMail::res_off(cap) + b] = ok ? 1 : 0;
+      reinterpret_cast<volatile uint8_t*>(base)[QcMail::res_off(cap) + b] = (uint8_t)ok;
     }
     __builtin_amdgcn_s_setprio(0);
   }
@@ -1737,7 +1744,7 @@ void launch_armed_w(const ArmArgs& a, hipStream_t st) {
         }
       }
       const uint32_t slots = a.slots >= 1 && a.slots <= QcMail::kQcSlots ? a.slots : QcMail::kQcSlots;
-      hipLaunchKernelGGL((k_ecdsa_rows_armed<WG, WQ>), dim3(slots), dim3(64 * kRowWaves), rl, st, a);
+      hipLaunchKernelGGL((k_ecdsa_rows_armed<WG, WQ>), dim3(slots), dim3(64 * RowsGeom<WG, WQ>::waves), rl, st, a);
       return;
     }
   }
@@ -1761,7 +1768,7 @@ void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* k
                           uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
   if constexpr (RowsGeom<WG, WQ>::ok) {
     if (n <= rows_max_batch() && rows_enabled()) {
-      hipLaunchKernelGGL((k_ecdsa_rows<WG, WQ>), dim3((uint32_t)n), dim3(64 * kRowWaves), 0, st, hashes, sigs, key_idx,
+      hipLaunchKernelGGL((k_ecdsa_rows<WG, WQ>), dim3((uint32_t)n), dim3(64 * RowsGeom<WG, WQ>::waves), 0, st, hashes, sigs, key_idx,
                          n, key_valid, nkeys, reinterpret_cast<const uint4*>(gtab),
                          reinterpret_cast<const uint4* const*>(qtabs), bitmap, okbytes);
       return;

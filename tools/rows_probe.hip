@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) rows_probe_k(const uint8_t* __
   bool key_ok = false;
   const uint4* qtab = nullptr;
   if (threadIdx.x < 64) wave_load_sig(hashes, sigs, key_idx, i, key_valid, nkeys, qtabs, e, r, s, key_ok, qtab);
-  const bool ok = block_verify_rows<WG, WQ>(e, r, s, key_ok, gtab, qtab, &sh);
+  const bool ok = block_verify_rows<WG, WQ, true>(e, r, s, key_ok, gtab, qtab, &sh) == 1;
   if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, nullptr);
 }
 
@@ -97,7 +97,7 @@ int main() {
   printf("{\"geometry\": [%d, %d]", WG, WQ);
   for (uint32_t nb : {1u, 3u, 64u}) {
     for (int rep = 0; rep < 4; ++rep) {
-      hipLaunchKernelGGL(rows_probe_k, dim3(nb), dim3(64 * kRowWaves), 0, 0, dh, ds, dk, (uint64_t)nb, dvalid, 1u,
+      hipLaunchKernelGGL(rows_probe_k, dim3(nb), dim3(64 * RowsGeom<WG, WQ>::waves), 0, 0, dh, ds, dk, (uint64_t)nb, dvalid, 1u,
                          reinterpret_cast<const uint4*>(gt), reinterpret_cast<const uint4* const*>(dq), dbm);
       CHECK(hipDeviceSynchronize());
     }
