@@ -1610,11 +1610,12 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
   }
 }
 
-// The narrow armed server on the row schedule: one 512-thread workgroup per
-// slot.  Wave 0 is the slot wave of k_ecdsa_wave_armed (the same polls,
-// exits, live / expired words and verdict store); the other seven wait at the
-// workgroup barrier -- they issue nothing while they wait -- and join
-// block_verify_rows when wave 0 has a signature for the slot.
+// The armed server on the row schedule: one workgroup (RowsGeom::waves waves)
+// per signature slot.  Wave 0 is the slot wave of k_ecdsa_wave_armed (the same
+// polls, exits, live / expired words and verdict store) -- or, in the wide
+// kernel (kQcCap workgroups, a relay), a helper wave for slots >= kQcSlots; the
+// other waves wait at the workgroup barrier -- they issue nothing while they
+// wait -- and join block_verify_rows when wave 0 has a signature for the slot.
 template <int WG, int WQ>
 __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) {
   __shared__ RowsShared sh;
@@ -1637,14 +1638,50 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
   }
   const uint4* gtab = reinterpret_cast<const uint4*>(a.gtab);
   const uint4* const* qtabs = reinterpret_cast<const uint4* const*>(a.qtabs);
-  const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b));
+  const bool helper = b >= QcMail::kQcSlots;  // (wide kernel only)
+  uint64_t* const relay = a.relay;
+  uint32_t last = 0;  // a helper's last relayed request (the relay starts at {0, 0}; numbers are never 0)
+  const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(helper ? 0 : b));
   const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
   for (;; ++want) {
     uint32_t e[8] = {}, r[8] = {}, s[8] = {};
     bool key_ok = false;
     const uint4* qtab = nullptr;
     uint64_t seen_wall = 0, seen_clk = 0;
-    if (wv == 0) {
+    if (wv == 0 && helper) {
+      // ---- a helper workgroup's wave 0: wave 0 of workgroup 0 relays each
+      // request's number and n through uncached device memory (see
+      // k_ecdsa_wave_armed); a slot below n reads its signature from the
+      // mailbox arrays in one round trip
+      uint64_t rv = 0;
+      for (;;) {
+        rv = __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)rv != last || wall_clock64() - t0 > a.budget) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      const uint32_t seq = (uint32_t)rv, n = (uint32_t)(rv >> 32);
+      uint32_t c = 0;
+      if (seq != last && n != 0xFFFFFFFFu) {
+        last = seq;
+        c = b < n ? 1u : 2u;
+        if (c == 1u) {
+          seen_wall = wall_clock64();
+          seen_clk = clock64();
+          constexpr uint32_t cap = QcMail::kQcCap;
+          const uint32_t* src = lane < 8    ? reinterpret_cast<const uint32_t*>(base + QcMail::hashes_off(cap) + 32 * b) + lane
+                                : lane < 24 ? reinterpret_cast<const uint32_t*>(base + QcMail::sigs_off(cap) + 64 * b) + (lane - 8)
+                                            : reinterpret_cast<const uint32_t*>(base + QcMail::keys_off(cap) + 4 * b);
+          const uint32_t v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          PBFTV_UNROLL for (int t = 0; t < 8; ++t) {
+            e[7 - t] = bswap32(__builtin_amdgcn_readlane(v, t));
+            r[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 8 + t));
+            s[7 - t] = bswap32(__builtin_amdgcn_readlane(v, 16 + t));
+          }
+          armed_key(__builtin_amdgcn_readlane(v, 24), nkeys, qt_lo, qt_hi, kv_lo, kv_hi, a.key_valid, qtabs, key_ok, qtab);
+        }
+      }
+      if (lane == 0) cmd = c;
+    } else if (wv == 0) {
       uint32_t v = 0;
       bool serve = false;
       for (;;) {
@@ -1670,11 +1707,15 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
       }
       uint32_t c = 0;
       if (!serve) {
+        if (b == 0 && relay && lane == 0)  // the helpers leave with workgroup 0
+          __hip_atomic_store(relay, ((uint64_t)0xFFFFFFFFu << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (lane == 0) __hip_atomic_store(mail->expired(a.slot), want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
         seen_wall = wall_clock64();
         seen_clk = clock64();
         const uint32_t n = __builtin_amdgcn_readlane(v, 1);
+        if (b == 0 && relay && n > QcMail::kQcSlots && lane == 0)
+          __hip_atomic_store(relay, ((uint64_t)n << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         c = b < n ? 1u : 2u;
         if (c == 1u) {
           const uint32_t k = __builtin_amdgcn_readlane(v, 2);
@@ -1733,7 +1774,7 @@ void launch_armed_w(const ArmArgs& a, hipStream_t st) {
   const bool wide = a.relay != nullptr;
   const bool excl = e && (e[0] == '1' || (!wide && e[0] == 'n'));
   if constexpr (RowsGeom<WG, WQ>::ok) {
-    if (!wide && rows_enabled()) {
+    if (rows_enabled()) {
       const uint32_t rl = excl ? 160u * 1024u - 4096u : 0u;  // (+ the kernel's static LDS)
       if (rl) {
         static bool rattr = false;
@@ -1743,7 +1784,7 @@ void launch_armed_w(const ArmArgs& a, hipStream_t st) {
           rattr = true;
         }
       }
-      const uint32_t slots = a.slots >= 1 && a.slots <= QcMail::kQcSlots ? a.slots : QcMail::kQcSlots;
+      const uint32_t slots = wide ? QcMail::kQcCap : a.slots >= 1 && a.slots <= QcMail::kQcSlots ? a.slots : QcMail::kQcSlots;
       hipLaunchKernelGGL((k_ecdsa_rows_armed<WG, WQ>), dim3(slots), dim3(64 * RowsGeom<WG, WQ>::waves), rl, st, a);
       return;
     }
