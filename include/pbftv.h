@@ -120,9 +120,16 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
  *                             on this hardware; off by default;
  *   PBFTV_QC_EXCLUSIVE_CU     armed workgroups take whole CUs, so a
  *                             concurrent batch does not share their SIMDs
- *                             (with PBFTV_QC_YIELD=0): "narrow" the 8-wave
- *                             kernel (2 CUs), "1" the 128-wave one too (32
- *                             CUs); off by default;
+ *                             (with PBFTV_QC_YIELD=0): "narrow" the narrow
+ *                             kernel (one CU per armed slot), "1" the wide
+ *                             one too (128 CUs); off by default;
+ *   PBFTV_QC_ROWS=0           the quad schedule (one wave per signature)
+ *                             instead of the row schedule (a workgroup per
+ *                             signature), for A/B;
+ *   PBFTV_QC_ROWS_MAX         launched batches up to this many signatures
+ *                             take the row schedule (default 128);
+ *   PBFTV_QC_SLOTS=k          arm k narrow slots (1..8) instead of the
+ *                             largest recent certificate (at least 4);
  *   PBFTV_QC_STAMPS=1         the kernel records GPU timestamps
  *                             (pbftv_qc_stamps*).
  * pbftv_dev_free / pbftv_host_free and the library's own frees stop every
