@@ -1247,14 +1247,22 @@ __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint
       return 2;
     }
   }
-  if (2 * wv >= nW) return 0;  // no window (its partners know that statically)
+  // Tree position t of this wave.  Waves w and w + 4 share a SIMD, and the
+  // older one takes its issue slots first: the younger runs when the older
+  // waits.  With six waves (11 or 12 windows) positions 4 and 5 are swapped,
+  // so the root (the longest chain: its pair, two levels, the fused check)
+  // shares SIMD 0 with the lightest position (5: one window for 11) and
+  // position 4 (a pair and one level) gets SIMD 1 once position 1 has handed
+  // its pair over.
+  const int t = RowsGeom<WG, WQ>::waves == 6 ? (wv == 4 ? 5 : wv == 5 ? 4 : wv) : wv;
+  if (2 * t >= nW) return 0;  // no window (its partners know that statically)
   const RowCtx c = row_ctx();
   const uint32_t rml = c.L < 9 ? sh->rm[c.L] : 0u;
   PBFTV_RPROBE(2, rml);
   // digits of every window (quad q = window q), each row pair keeps its own
   const int q = lane >> 2;
   const int d1 = lane_window_digit<WG>(u1, q), d2 = lane_window_digit<WQ>(u2, q);
-  const int wA = 2 * wv, wB = 2 * wv + 1;
+  const int wA = 2 * t, wB = 2 * t + 1;
   const int a1 = __builtin_amdgcn_readlane(d1, 4 * wA), a2 = __builtin_amdgcn_readlane(d2, 4 * wA);
   const int b1 = __builtin_amdgcn_readlane(d1, 4 * wB), b2 = __builtin_amdgcn_readlane(d2, 4 * wB);
   const bool pb = c.row >= 2;
@@ -1298,27 +1306,27 @@ __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint
   // wave whose subtree is ready early goes on while slower ones still add.
   bool ok = false, exc = false;
   PBFTV_UNROLL for (int m = 1; m < kRowWaves; m <<= 1) {
-    if ((wv & (2 * m - 1)) == m) {
+    if ((t & (2 * m - 1)) == m) {
       if (c.row == 0) {
-        sh->pts[wv][0][c.L] = P.x;
-        sh->pts[wv][1][c.L] = P.y;
-        sh->pts[wv][2][c.L] = P.zz;
-        sh->pts[wv][3][c.L] = P.zzz;
+        sh->pts[t][0][c.L] = P.x;
+        sh->pts[t][1][c.L] = P.y;
+        sh->pts[t][2][c.L] = P.zz;
+        sh->pts[t][3][c.L] = P.zzz;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&sh->ready[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) __hip_atomic_store(&sh->ready[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return 0;
     }
-    if (2 * (wv + m) < nW) {  // add the partner's
-      while (__hip_atomic_load(&sh->ready[wv + m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+    if (2 * (t + m) < nW) {  // add the partner's
+      while (__hip_atomic_load(&sh->ready[t + m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       PBFTV_RPROBE(5 + 2 * m - (m == 4 ? 1 : 0), m);
       xyzz_r Q;
-      Q.x = sh->pts[wv + m][0][c.L];
-      Q.y = sh->pts[wv + m][1][c.L];
-      Q.zz = sh->pts[wv + m][2][c.L];
-      Q.zzz = sh->pts[wv + m][3][c.L];
+      Q.x = sh->pts[t + m][0][c.L];
+      Q.y = sh->pts[t + m][1][c.L];
+      Q.zz = sh->pts[t + m][2][c.L];
+      Q.zzz = sh->pts[t + m][3][c.L];
       if (m == kRowWaves / 2) {  // wave 0: the last level, fused with the check
         ok = xyzz_add_check_rows(c, exc, P, Q, rz);
       } else {
@@ -1327,7 +1335,7 @@ __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint
     }
     PBFTV_RPROBE(6 + 2 * m - (m == 4 ? 1 : 0), P.y ^ (uint32_t)ok);
   }
-  if (wv != 0) return 0;
+  if (t != 0) return 0;
   exc = exc || (sh->ctl & 4u) != 0;
   if (exc) {  // a doubling / cancellation somewhere, or a rare window: exact rerun
     if constexpr (kExact) {
