@@ -67,8 +67,9 @@ int fail(int code, const std::string& msg) {
 // the mailbox words are host memory and the halt bump is one atomic add.
 struct ArmRegistry {
   std::mutex mu;
-  std::map<int, std::vector<pbftv::QcMail*>> mail;  // GPU -> registered mailboxes
-  std::map<int, int> quiesce;                       // GPU -> quiesces in progress
+  std::map<int, std::vector<pbftv::QcMail*>> mail;              // GPU -> registered mailboxes
+  std::map<int, std::vector<std::condition_variable*>> keepers;  // GPU -> their devices' keeper wake-ups
+  std::map<int, int> quiesce;                                   // GPU -> quiesces in progress
 };
 ArmRegistry& arm_registry() {
   static ArmRegistry* r = new ArmRegistry;  // never destroyed: DevBuf destructors may run at exit
@@ -96,6 +97,11 @@ struct GpuQuiesce {
     ArmRegistry& r = arm_registry();
     std::lock_guard<std::mutex> lk(r.mu);
     --r.quiesce[gpu];
+    // the halted servers' keepers re-arm now, not at their next half budget
+    // (a certificate in between would take a launch)
+    for (auto& kv : r.keepers)
+      if ((gpu < 0 || kv.first == gpu) && arming_allowed_locked(r, kv.first))
+        for (std::condition_variable* cv : kv.second) cv->notify_one();
   }
   GpuQuiesce(const GpuQuiesce&) = delete;
   GpuQuiesce& operator=(const GpuQuiesce&) = delete;
@@ -434,6 +440,7 @@ void qc_register(Device& d) {
   ArmRegistry& r = arm_registry();
   std::lock_guard<std::mutex> lk(r.mu);
   r.mail[d.id].push_back(qc_mail(d));
+  r.keepers[d.id].push_back(&d.keeper_cv);
   d.mail_registered = true;
 }
 
@@ -443,6 +450,8 @@ void qc_unregister(Device& d) {
   std::lock_guard<std::mutex> lk(r.mu);
   auto& v = r.mail[d.id];
   v.erase(std::remove(v.begin(), v.end(), qc_mail(d)), v.end());
+  auto& k = r.keepers[d.id];
+  k.erase(std::remove(k.begin(), k.end(), &d.keeper_cv), k.end());
   d.mail_registered = false;
 }
 
@@ -651,7 +660,8 @@ void qc_keeper_loop(Device* d) {
     } else if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
       // also re-arms after a disarm (key change) or a halt (quiesce)
       const bool reshape = d->arm_seq && (d->arm_waves == kQcCap) != qc_wide_wanted(*d);
-      if (d->arm_seq == 0 || now >= d->armed_at + half || reshape) {
+      const bool left = d->arm_seq && __atomic_load_n(qc_mail(*d)->expired(d->arm_stream), __ATOMIC_ACQUIRE) == d->arm_seq;
+      if (d->arm_seq == 0 || now >= d->armed_at + half || reshape || left) {  // (left: halted by a quiesce)
         if (qc_rotate(*d) != hipSuccess) (void)hipGetLastError();  // a call will launch instead
         ++d->rotations;
       }

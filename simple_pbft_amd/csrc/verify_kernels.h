@@ -1060,7 +1060,9 @@ __device__ __forceinline__ void fe_readlane(fe& d, const fe& s, int lane) {
 __device__ __forceinline__ void wave_scalars(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
                                              uint32_t u1[8], uint32_t u2[8], fe& rm, fe& rnm, bool& rn_ok) {
   fe D;
+  PBFTV_RPROBE(15, s[0]);
   inv_mod_n_wave(D, s);
+  PBFTV_RPROBE(14, D.v[0]);
   uint32_t rn[8];
   uint64_t cy = 0;
   PBFTV_UNROLL for (int i = 0; i < 8; ++i) {
@@ -1094,6 +1096,43 @@ __device__ __forceinline__ void wave_scalars(const uint32_t e[8], const uint32_t
   }
   fe_readlane(rm, prod, 2);
   fe_readlane(rnm, prod, 3);
+}
+
+// The same scalars for the row schedule, written by the lanes that computed
+// them straight into the workgroup's LDS (lane 0: u1, lane 1: u2, lane 2:
+// r R mod p as 29-bit limbs) -- no readlane of the 25 words and no per-lane
+// select, ~1 µs of a lone wave's issue.  u1, u2 get one reduction step, to
+// [0, 2^256): u and u - n give the same comb sum.
+__device__ __forceinline__ void wave_scalars_lds(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
+                                                 uint32_t* u1, uint32_t* u2, uint32_t* rm) {
+  fe D;
+  PBFTV_RPROBE(15, s[0]);
+  inv_mod_n_wave(D, s);
+  PBFTV_RPROBE(14, D.v[0]);
+  const int role = (int)(threadIdx.x & 3u);
+  fe ev, rv, a, b, m, r2p, nmod, pmod, prod;
+  fe_from_words(ev, e);
+  fe_from_words(rv, r);
+  fe_set(r2p, kR2P);
+  fe_set(nmod, kN);
+  fe_set(pmod, kP);
+  const bool modn = role < 2;
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) {
+    a.v[l] = role == 0 ? ev.v[l] : rv.v[l];
+    b.v[l] = modn ? D.v[l] : r2p.v[l];
+    m.v[l] = modn ? nmod.v[l] : pmod.v[l];
+  }
+  fmont_lane(prod, a, b, m, modn ? kNPrime : 1u);  // lanes 0, 1: e D, r D mod n; lane 2: r R mod p
+  const int lane = (int)(threadIdx.x & 63u);
+  if (lane < 2) {
+    fn_canon(a, prod);  // < 2^256 + n  ->  < 2^256
+    uint32_t w[8];
+    fe_to_words(w, a);
+    uint32_t* dst = lane == 0 ? u1 : u2;
+    PBFTV_UNROLL for (int k = 0; k < 8; ++k) dst[k] = w[k];
+  } else if (lane == 2) {
+    PBFTV_UNROLL for (int l = 0; l < 9; ++l) rm[l] = prod.v[l];
+  }
 }
 
 // x(P) == r or r + n (mod n) for the all-reduced XYZZ sum: lanes 0 and 1 test
@@ -1203,21 +1242,8 @@ __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint
   if (wv == 0) {
     uint32_t ctl = 0;
     if (key_ok && !words_is_zero(r) && !words_is_zero(s) && words_lt(r, kN32) && words_lt(s, kN32)) {
-      uint32_t u1[8], u2[8];
-      fe rm, rnm;
-      bool rn_ok;
-      wave_scalars(e, r, s, u1, u2, rm, rnm, rn_ok);
-      ctl = rn_ok ? 3u : 1u;
-      uint32_t a = 0, b = 0;
-      PBFTV_UNROLL for (int k = 0; k < 8; ++k) {
-        a = lane == k ? u1[k] : a;
-        b = lane == k ? u2[k] : b;
-      }
-      if (lane < 8) {
-        sh->u1[lane] = a;
-        sh->u2[lane] = b;
-      }
-      if (lane < 9) sh->rm[lane] = limb_of(rm.v, lane);
+      wave_scalars_lds(e, r, s, sh->u1, sh->u2, sh->rm);
+      ctl = words_lt(r, kPMinusN32) ? 3u : 1u;  // r + n < p: the exact path
       if (lane == 0) sh->qtab = (uint64_t)(uintptr_t)qtab;
     }
     if (lane == 0) sh->ctl = ctl;

@@ -561,7 +561,7 @@ def test_armed_latency_path(oracle_lib, mode, monkeypatch):
         if mode == "keeper":
             # the keeper kept one armed through every pause -- after the first
             # 67-signature call a WIDE one (helper waves serve up to 128)
-            assert all(a for _, _, a in served), served
+            assert all(a for _, _, a in served), [x for x in served if not x[2]]
         else:
             assert not any(a for _, _, a in served), served  # every one expired: launched instead
         # a key change while a kernel is armed: it is cancelled first

@@ -119,6 +119,19 @@ int main() {
     for (uint32_t b = 0; b < nb && b < 128; ++b) tot.push_back((double)(st[b * 8 * kS + 13] - st[b * 8 * kS]) * 1e3 / rate_khz);
     std::sort(tot.begin(), tot.end());
     printf(", \"total_us\": %.2f", tot[tot.size() / 2]);
+    {  // wave 0 inside the scalars: entry -> inversion start (15) -> inversion end (14) -> scalars done (1)
+      std::vector<double> a, b, c;
+      for (uint32_t k = 0; k < nb && k < 128; ++k) {
+        const uint64_t* s = &st[k * 8 * kS];
+        a.push_back((double)(s[15] - s[0]) * 1e3 / rate_khz);
+        b.push_back((double)(s[14] - s[15]) * 1e3 / rate_khz);
+        c.push_back((double)(s[1] - s[14]) * 1e3 / rate_khz);
+      }
+      std::sort(a.begin(), a.end());
+      std::sort(b.begin(), b.end());
+      std::sort(c.begin(), c.end());
+      printf(", \"scalars_split_us\": [%.2f, %.2f, %.2f]", a[a.size() / 2], b[b.size() / 2], c[c.size() / 2]);
+    }
     // workgroup 0, every wave: handoff end (2) -> entries (3) -> level 0 (4) -> pair add (5), from wave 0's stamp 2
     printf(", \"wg0_waves_us_since_handoff\": [");
     for (int w = 0; w < 8; ++w) {
