@@ -577,6 +577,40 @@ def test_armed_latency_path(oracle_lib, mode, monkeypatch):
         assert armed >= (190 if mode == "keeper" else 0)
 
 
+def test_armed_slots_follow_certificate_size(oracle_lib, monkeypatch):
+    """The narrow row-schedule server arms one workgroup per slot: as many
+    slots as the largest certificate of the last period, at least 4.  A
+    7-signature certificate after 3-signature ones is served by a launch (the
+    armed kernel has 4 slots) and re-arms with 7 at once, so the next 7s are
+    armed; every bitmap and quorum count against the oracle, with corrupted
+    votes in every certificate."""
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_WIDE", "0")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=8, per_key=12, seed=91)
+    sigs[::4, 50] ^= 0x04
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    rng = np.random.default_rng(92)
+    served = []
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        for it, n in enumerate([3, 3, 3, 7, 7, 7, 7, 2, 8, 8, 1]):
+            o = rng.choice(n_all, n, replace=False)
+            bm, acc, ok = v.qc_verify(hashes[o], sigs[o], kidx[o], quorum=n)
+            assert (bm == want[o]).all() and acc == int(want[o].sum()), (it, n)
+            served.append((it, n, v.qc_stamps(0)["armed"]))
+            time.sleep(0.005)
+    armed = {it: a for it, _, a in served}
+    assert all(armed[it] for it in (1, 2)), served        # 3 <= 4 slots
+    assert not armed[3], served                             # 7 > 4: launched, re-armed wider
+    assert all(armed[it] for it in (4, 5, 6, 7)), served  # 7 slots now
+    assert not armed[8] and armed[9] and armed[10], served  # 8 > 7: once launched
+
+
 def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypatch):
     """An armed kernel with a 5-s budget stays resident between calls.  A
     device free and a pinned-host free must not wait for it: the library
