@@ -1279,8 +1279,17 @@ __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint
   // so the root (the longest chain: its pair, two levels, the fused check)
   // shares SIMD 0 with the lightest position (5: one window for 11) and
   // position 4 (a pair and one level) gets SIMD 1 once position 1 has handed
-  // its pair over.
-  const int t = RowsGeom<WG, WQ>::waves == 6 ? (wv == 4 ? 5 : wv == 5 ? 4 : wv) : wv;
+  // its pair over.  With seven (13 or 14 windows) position 4 (a pair and two
+  // levels) takes wave 3, the one alone on its SIMD, the root shares SIMD 0
+  // with position 6 (one window for 13) and position 2 shares SIMD 2 with
+  // position 3, its own first partner.
+  constexpr int kWaves = RowsGeom<WG, WQ>::waves;
+  int t = kWaves == 6   ? (wv == 4 ? 5 : wv == 5 ? 4 : wv)
+                : kWaves == 7 ? (wv == 3 ? 4 : wv == 4 ? 6 : wv == 6 ? 3 : wv)
+                              : wv;
+#ifdef PBFTV_ROWS_IDENTITY  // (A/B only)
+  t = wv;
+#endif
   if (2 * t >= nW) return 0;  // no window (its partners know that statically)
   const RowCtx c = row_ctx();
   const uint32_t rml = c.L < 9 ? sh->rm[c.L] : 0u;

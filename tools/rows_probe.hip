@@ -18,7 +18,10 @@ using namespace pbftv;
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
-constexpr int WG = 29, WQ = 24;
+#ifndef PROBE_WQ
+#define PROBE_WQ 24
+#endif
+constexpr int WG = 29, WQ = PROBE_WQ;  // (-DPROBE_WQ=20: 13 windows, seven waves)
 
 // k_ecdsa_rows' body in a kernel of this unit (the library's objects carry
 // their own, unstamped, instantiation of the template)
