@@ -221,6 +221,9 @@ struct Device {
   uint32_t arm_waves = 0;                  // signatures the armed kernel serves: its slots (narrow) or kQcCap (wide)
   uint32_t qc_nmax = 0;                    // largest narrow certificate since the last arming
   uint32_t qc_slots = 4;                   // slots the next narrow arming takes (the row schedule: a CU each)
+  uint32_t qc_wmax = 0;                    // largest wide certificate (9..kQcCap) since the last arming
+  uint32_t qc_wslots = 0;                  // workgroups of the wide arming (grows while wide is wanted; 0: none yet)
+  bool arm_live = false;                   // every workgroup of the armed kernel has reported itself resident
   std::chrono::steady_clock::time_point last_wide{};  // the last latency-path call of 9..kQcCap signatures
   std::chrono::steady_clock::time_point armed_at{}, last_qc{};
   // diagnostics of the last latency-path call (pbftv_qc_stamps)
@@ -586,6 +589,19 @@ hipError_t qc_arm(Device& d) {
   const char* ke = getenv("PBFTV_QC_SLOTS");
   uint32_t slots = (re && re[0] == '0') ? QcMail::kQcSlots : d.qc_slots;
   if (ke && atoi(ke) >= 1 && atoi(ke) <= (int)QcMail::kQcSlots) slots = (uint32_t)atoi(ke);
+  // wide: one workgroup per signature of the largest certificate seen while
+  // wide ones keep coming, rounded up to 8 (a 67-vote certificate arms 72, not
+  // 128 -- the resident footprint is ~6 waves per workgroup); a larger one is
+  // launched once and the next arming is wider; it never shrinks until wide
+  // certificates stop (qc_wide_wanted)
+  if (relay) {
+    if (d.qc_wmax) d.qc_wslots = std::max(d.qc_wslots, std::min<uint32_t>(kQcCap, (d.qc_wmax + 7) / 8 * 8));
+    if (!d.qc_wslots) d.qc_wslots = kQcCap;
+  } else {
+    d.qc_wslots = 0;
+  }
+  d.qc_wmax = 0;
+  const uint32_t wslots = (re && re[0] == '0') ? kQcCap : d.qc_wslots;
   const char* se = getenv("PBFTV_QC_STAMPS");
   const ArmArgs a{qc_mail(d),
                   want,
@@ -599,10 +615,11 @@ hipError_t qc_arm(Device& d) {
                   relay,
                   se && se[0] == '1' ? 1u : 0u,
                   slot,
-                  slots};
+                  relay ? wslots : slots};
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = d.armed_first = want;
-  d.arm_waves = relay ? kQcCap : slots;
+  d.arm_waves = relay ? wslots : slots;
+  d.arm_live = false;
   d.arm_stream = slot;
   d.armed_at = std::chrono::steady_clock::now();
   if (!d.keeper.joinable() && qc_keep_ms() > 0) d.keeper = std::thread(qc_keeper_loop, &d);
@@ -630,12 +647,27 @@ hipError_t qc_rotate(Device& d) {
   return hipSuccess;
 }
 
+// every workgroup of the armed kernel resident (checked once per arming)
+bool qc_all_live(Device& d) {
+  if (d.arm_live) return true;
+  if (!d.arm_seq) return false;
+  const uint32_t* live = reinterpret_cast<const uint32_t*>(d.stage.as<uint8_t>() + QcMail::live_off(d.arm_stream));
+  for (uint32_t w = 0; w < d.arm_waves; ++w)
+    if (__atomic_load_n(live + w, __ATOMIC_ACQUIRE) != d.armed_first) return false;
+  d.arm_live = true;
+  return true;
+}
+
 // retire the rotated-out kernel once its successor is resident
+// (its slot workgroups, <= kQcSlots: a wide successor's helpers may find room
+// only once the predecessor has left -- two wide row kernels need up to 256
+// workgroups of ~6 waves -- and until they are all resident a wide
+// certificate is launched, qc_all_live)
 void qc_retire(Device& d) {
   if (!d.retiring || !d.arm_seq) return;
   const uint32_t* live = reinterpret_cast<const uint32_t*>(d.stage.as<uint8_t>() + QcMail::live_off(d.arm_stream));
-  for (uint32_t w = 0; w < d.arm_waves; ++w)
-    if (__atomic_load_n(live + w, __ATOMIC_ACQUIRE) != d.armed_first) return;  // not every wave resident yet
+  for (uint32_t w = 0; w < std::min<uint32_t>(d.arm_waves, QcMail::kQcSlots); ++w)
+    if (__atomic_load_n(live + w, __ATOMIC_ACQUIRE) != d.armed_first) return;  // not every slot resident yet
   __atomic_store_n(&qc_mail(d)->stop, d.retiring, __ATOMIC_RELEASE);
   d.retiring = 0;
 }
@@ -1832,14 +1864,32 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       return PBFTV_OK;
     };
     // an armed kernel that has left (budget, cancel, halt) is collected first
+    bool collected = false;
     if (d.arm_seq && __atomic_load_n(m->expired(d.arm_stream), __ATOMIC_ACQUIRE) == d.arm_seq) {
       HIP_TRY(set_dev());
       HIP_TRY(qc_disarm(d));
+      collected = true;
     }
+    static const bool trace_qc = getenv("PBFTV_TRACE") != nullptr;
+    if (trace_qc && small && d.arm_seq && n <= d.arm_waves && n > QcMail::kQcSlots && !qc_all_live(d)) {
+      const uint32_t* lv = reinterpret_cast<const uint32_t*>(d.stage.as<uint8_t>() + QcMail::live_off(d.arm_stream));
+      uint32_t k = 0;
+      for (uint32_t w = 0; w < d.arm_waves; ++w) k += __atomic_load_n(lv + w, __ATOMIC_ACQUIRE) == d.armed_first;
+      fprintf(stderr, "pbftv[dev %d] qc n=%llu launched: %u of %u workgroups of armed %u live (armed %.1f ms ago, retiring %u)\n",
+              d.id, (unsigned long long)n, k, d.arm_waves, d.arm_seq,
+              std::chrono::duration<double, std::milli>(h_in - d.armed_at).count(), d.retiring);
+    }
+    if (trace_qc && small && !(d.arm_seq && n <= d.arm_waves))  // (diagnostics: why a launch)
+      fprintf(stderr, "pbftv[dev %d] qc n=%llu launched: arm_seq=%u arm_waves=%u collected=%d wide_wanted=%d retiring=%u\n",
+              d.id, (unsigned long long)n, d.arm_seq, d.arm_waves, (int)collected, (int)qc_wide_wanted(d), d.retiring);
     uint32_t cur = 0;  // the armed request number serving this call
     if (n > QcMail::kQcSlots && small) d.last_wide = h_in;
     if (n <= QcMail::kQcSlots) d.qc_nmax = std::max(d.qc_nmax, (uint32_t)n);
-    if (d.arm_seq && n <= d.arm_waves) {
+    else if (small) d.qc_wmax = std::max(d.qc_wmax, (uint32_t)n);
+    // a wide certificate needs every helper workgroup resident: one that is
+    // still waiting for room on the GPU (beside other resident kernels) would
+    // start only after the armed kernel's budget, too late to serve
+    if (d.arm_seq && n <= d.arm_waves && (n <= QcMail::kQcSlots || qc_all_live(d))) {
       cur = d.arm_seq;
       if (n > QcMail::kQcSlots) {  // the helpers' inputs (slots kQcSlots..n-1), before any slot tag
         std::memcpy(st8 + QcMail::hashes_off(cap) + 32 * QcMail::kQcSlots, hashes + 32 * QcMail::kQcSlots,
@@ -1880,7 +1930,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       if (rc != PBFTV_OK) return rc;
       if (small) {
         if (d.arm_seq && n > d.arm_waves && (qc_wide_wanted(d) || n <= QcMail::kQcSlots))
-          HIP_TRY(qc_rotate(d));  // wide, or more narrow slots (qc_nmax), for the next one
+          HIP_TRY(qc_rotate(d));  // wide, or more slots (qc_nmax / qc_wmax), for the next one
         HIP_TRY(qc_arm(d));  // the next call's server (no-op while one is armed)
       }
     }
@@ -1898,6 +1948,11 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       if (cur && __atomic_load_n(m->expired(d.arm_stream), __ATOMIC_ACQUIRE) == cur) {
         // the armed kernel left (budget, cancel, halt) before it saw the bell:
         // wait for the armed kernels to leave, then launch
+        if (trace_qc)
+          fprintf(stderr, "pbftv[dev %d] qc n=%llu: armed %u left unserved after %.1f us (halt %u, stop %u, armed %.1f ms ago)\n",
+                  d.id, (unsigned long long)n, cur,
+                  std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h_in).count(), m->halt,
+                  m->stop, std::chrono::duration<double, std::milli>(h_in - d.armed_at).count());
         HIP_TRY(set_dev());
         HIP_TRY(qc_disarm(d));
         cur = 0;
@@ -1920,6 +1975,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         bool missing = false;
         for (uint64_t i = next; i < n; ++i) missing |= res[i] == 0xFF;
         if (!missing) break;
+        if (trace_qc) fprintf(stderr, "pbftv[dev %d] qc n=%llu: 2-s timeout, armed %u\n", d.id, (unsigned long long)n, cur);
         if (cur) {
           // an armed server that left without its exit being seen (no fault:
           // the streams synchronised cleanly) is a lost doorbell, not a device

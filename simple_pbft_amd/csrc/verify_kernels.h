@@ -883,19 +883,12 @@ __device__ __forceinline__ uint32_t lane_limb(const uint32_t v[9], int L) {
 __device__ __forceinline__ void inv_mod_n_wave(fe& D, const uint32_t x[8]) {
   const int lane = (int)(threadIdx.x & 63u), L = lane & 15, row = lane >> 4;
   const bool act = L < 9 && row < 2, top = L == 8;
-  s30 xs, rn;
+  s30 xs;
   words_to_s30(xs, x);
-  {
-    uint32_t rw[8];  // R mod n = 2^261 mod n as words: from kOneN (R mod n in 29-bit limbs)
-    fe one;
-    fe_set(one, kOneN);
-    fe_to_words(rw, one);
-    words_to_s30(rn, rw);
-  }
   const uint32_t nl = act && row == 1 ? lane_limb(kN30, L) : 0u;
   int32_t A = act && row == 0 ? (int32_t)lane_limb(kN30, L) : 0;                         // f = n, d = 0
   const uint32_t xl = lane_limb(reinterpret_cast<const uint32_t*>(xs.v), L);
-  const uint32_t rl = lane_limb(reinterpret_cast<const uint32_t*>(rn.v), L);
+  const uint32_t rl = lane_limb(kRN30, L);  // R mod n = 2^261 mod n
   int32_t B = act ? (int32_t)(row == 0 ? xl : rl) : 0;  // g = x, e = R mod n
   A = limbs_center(A, top);
   B = limbs_center(B, top);
@@ -1827,7 +1820,8 @@ void launch_armed_w(const ArmArgs& a, hipStream_t st) {
           rattr = true;
         }
       }
-      const uint32_t slots = wide ? QcMail::kQcCap : a.slots >= 1 && a.slots <= QcMail::kQcSlots ? a.slots : QcMail::kQcSlots;
+      const uint32_t cap = wide ? QcMail::kQcCap : QcMail::kQcSlots;
+      const uint32_t slots = a.slots >= (wide ? QcMail::kQcSlots + 1 : 1) && a.slots <= cap ? a.slots : cap;
       hipLaunchKernelGGL((k_ecdsa_rows_armed<WG, WQ>), dim3(slots), dim3(64 * RowsGeom<WG, WQ>::waves), rl, st, a);
       return;
     }

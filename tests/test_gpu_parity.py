@@ -560,8 +560,18 @@ def test_armed_latency_path(oracle_lib, mode, monkeypatch):
             time.sleep(0.06)  # three budgets (keeper) / sixty (expiring)
         if mode == "keeper":
             # the keeper kept one armed through every pause -- after the first
-            # 67-signature call a WIDE one (helper waves serve up to 128)
-            assert all(a for _, _, a in served), [x for x in served if not x[2]]
+            # 67-signature call a WIDE one, with a workgroup per signature of
+            # the largest wide certificate so far (rounded up to 8): a larger
+            # one is launched once and the next arming is wider
+            wide_max, expect = 67, []
+            for it, n, a in served:
+                if 8 < n <= 128 and n > (wide_max + 7) // 8 * 8:
+                    expect.append((it, n, False))
+                else:
+                    expect.append((it, n, True))
+                if 8 < n <= 128:
+                    wide_max = max(wide_max, n)
+            assert served == expect, [(x, y) for x, y in zip(served, expect) if x != y]
         else:
             assert not any(a for _, _, a in served), served  # every one expired: launched instead
         # a key change while a kernel is armed: it is cancelled first
