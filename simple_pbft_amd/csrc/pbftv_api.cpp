@@ -699,7 +699,7 @@ void qc_keeper_loop(Device* d) {
       }
       wake = d->arm_seq ? std::min(d->armed_at + half, d->last_qc + keep) : now + std::chrono::milliseconds(1);
     }
-    if (d->retiring) wake = std::min(wake, now + std::chrono::milliseconds(1));
+    if (d->retiring) wake = std::min(wake, now + std::chrono::microseconds(100));  // (a wide successor waits for its room)
     if (wake <= now) wake = now + std::chrono::milliseconds(1);
     d->keeper_idle = wake - now > std::chrono::minutes(1);  // a call wakes it (d.last_qc moved)
     d->keeper_cv.wait_until(lk, wake);
