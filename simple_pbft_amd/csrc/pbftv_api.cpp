@@ -643,6 +643,14 @@ hipError_t qc_rotate(Device& d) {
   if (old) {
     if (d.retiring) __atomic_store_n(&qc_mail(d)->stop, d.retiring, __ATOMIC_RELEASE);  // (not live yet: rare)
     d.retiring = old;
+    if (d.arm_waves > QcMail::kQcSlots) {
+      // a wide successor (up to 128 workgroups of ~6 waves) may not find room
+      // beside its predecessor -- and beside other contexts' servers -- so
+      // the predecessor leaves at once instead of overlapping (a wide
+      // certificate in the gap is launched: qc_all_live)
+      __atomic_store_n(&qc_mail(d)->stop, old, __ATOMIC_RELEASE);
+      d.retiring = 0;
+    }
   }
   return hipSuccess;
 }
