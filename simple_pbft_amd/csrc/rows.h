@@ -200,8 +200,17 @@ __device__ __forceinline__ bool xyzz_add_check_rows(const RowCtx& c, bool& exc, 
   const uint32_t w = U1 + U2 + rz12;  // = P + 2 U1 + r ZZ1 ZZ2; limbs < 3 (2^29 + 2^5)
   m = row_mul(c, c.row & 1 ? P : PP, c.row & 1 ? rz12 : w);
   gather4(g, m);  // PP (P + 2 U1 + r ZZ12); P r ZZ1 ZZ2, zero iff either factor is (p prime)
-  exc = row_is_zero(g[1]);
-  return row_is_zero(R2 - g[0]);
+  // both zero tests at once, half a wave each: lanes 0-31 the check's
+  // difference, lanes 32-63 the exceptional product
+  fe a, b, x;
+  row_to_fe(a, R2 - g[0]);
+  row_to_fe(b, g[1]);
+  const bool hi = (threadIdx.x & 63u) >= 32u;
+  PBFTV_UNROLL for (int l = 0; l < 9; ++l) x.v[l] = hi ? b.v[l] : a.v[l];
+  fs_norm(x, x);
+  const uint64_t z = __ballot(fs_is_zero(x));
+  exc = ((z >> 32) & 1u) != 0;
+  return (z & 1u) != 0;
 }
 
 }  // namespace pbftv
