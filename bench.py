@@ -341,6 +341,25 @@ def in_context_leg(ws: int, share: bool, pub, H, S, K, ok, steps: int, warmup_ms
     return out
 
 
+def in_context_result(ws: int, leg) -> tuple[dict, str | None]:
+    """Run the in_context leg (leg() -> its dict) and judge it: an exception,
+    a context that does not span --gpus devices, or a failed bitmap check is a
+    failure of the product's own multi-device path, and bench.py then exits
+    non-zero after printing its line (the driver's 8-GPU run
+    must not report a green line over a broken run_sharded).  Returns
+    (the leg's dict, the failure or None)."""
+    try:
+        res = leg()
+    except Exception as e:  # noqa: BLE001 -- reported in the line AND in the exit status
+        return {"error": repr(e)}, f"in_context raised {e!r}"
+    if len(res.get("devices", [])) != ws:
+        return res, f"in_context ran on {len(res.get('devices', []))} devices, --gpus {ws}"
+    for part in ("host_path", "device_resident"):
+        if not res.get(part, {}).get("check", False):
+            return res, f"in_context {part} bitmap check failed"
+    return res, None
+
+
 class Dist:
     def __init__(self, ws):
         self.ws = ws
@@ -996,14 +1015,32 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} rank processes: launch with "
                          f"--nproc-per-node {args.gpus}, or without torch.distributed.run")
     d = Dist(ws)
-    if os.environ.get("PBFTV_BENCH_PROBE") == "1":
-        # launcher check without a GPU (tests/test_dist.py): the ranks that came up
+    probe = os.environ.get("PBFTV_BENCH_PROBE")
+    if probe:
+        # launcher check without a GPU (tests/test_dist.py): the ranks that came
+        # up; "in_context:<stub>" also runs rank 0's in_context judgement on a
+        # stub leg ("raise", "devices": one device short, "check": a failed
+        # bitmap, "ok") -- the exit status the driver would see
         seen = d.sum(1.0)
+        failure = None
+        line = {"probe": True, "world_size": ws, "ranks_seen": seen, "gpus": args.gpus,
+                "spawned": os.environ.get("PBFTV_BENCH_SPAWNED") == "1",
+                "shared_data": os.environ.get("PBFTV_BENCH_DATA") is not None}
+        if rank == 0 and probe.startswith("in_context:"):
+            stub = probe.split(":", 1)[1]
+
+            def leg():
+                if stub == "raise":
+                    raise RuntimeError("stub in_context leg failed")
+                devs = list(range(ws - 1 if stub == "devices" else ws))
+                return {"devices": devs, "host_path": {"check": True}, "device_resident": {"check": stub != "check"}}
+            line["in_context"], failure = in_context_result(ws, leg)
         if rank == 0:
-            print(json.dumps({"probe": True, "world_size": ws, "ranks_seen": seen, "gpus": args.gpus,
-                              "spawned": os.environ.get("PBFTV_BENCH_SPAWNED") == "1",
-                              "shared_data": os.environ.get("PBFTV_BENCH_DATA") is not None}), flush=True)
+            print(json.dumps(line), flush=True)
+        d.barrier()
         d.close()
+        if failure:
+            raise SystemExit(f"bench.py: {failure}")
         return
     # one GPU per rank; PBFTV_BENCH_SHARE_DEVICE=1 puts every rank on device 0
     # (only to rehearse the N > 1 flow on a 1-GPU box -- not a scaling number)
@@ -1261,15 +1298,18 @@ def main():
             ver.stream_destroy(0, st)
     ver.close()  # every rank's tables leave HBM before the one-context leg builds its own
     d.barrier()
+    failure = None
     if rank == 0 and ws > 1 and glob is not None and not args.no_in_context:
-        try:
-            out["in_context"] = in_context_leg(ws, share, *glob, steps=args.steps, warmup_ms=args.warmup_ms)
-        except Exception as e:  # noqa: BLE001 -- reported in the line; the per-rank value above stands
-            out["in_context"] = {"error": repr(e)}
+        out["in_context"], failure = in_context_result(
+            ws, lambda: in_context_leg(ws, share, *glob, steps=args.steps, warmup_ms=args.warmup_ms))
+        if failure:
+            out["in_context_check"] = "FAIL"
     if rank == 0:
         print(json.dumps(out), flush=True)
     d.barrier()
     d.close()
+    if failure:
+        raise SystemExit(f"bench.py: {failure}")
 
 
 if __name__ == "__main__":

@@ -165,6 +165,15 @@ int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]);
  * helper waves past the 8 slots included): returns the number written, 0 if a
  * launch served the call.  Stamps of waves that had no signature are stale. */
 int pbftv_qc_stamps_all(pbftv_ctx* ctx, int dev, uint64_t* out, uint32_t waves);
+/* Counters of the latency path on device dev since pbftv_open (diagnostics;
+ * tests assert which path served what): out[0] calls, out[1] calls served by
+ * an armed kernel, out[2] armed calls handed to a launched rerun (the armed
+ * row kernel met an exceptional signature: a doubling or cancellation in its
+ * tree, a live window with two zero digits, r + n < p), out[3] signatures that
+ * took a launched row kernel's exact path, out[4] launched latency kernels,
+ * out[5] armings, out[6] keeper rotations, out[7] the armed kernel now: its
+ * workgroups (0: none armed) | 1 << 32 if it is the wide one. */
+int pbftv_qc_counters(pbftv_ctx* ctx, int dev, uint64_t out[8]);
 
 /* ---- SHA-256 digests (utils.Hash) ------------------------------------ */
 

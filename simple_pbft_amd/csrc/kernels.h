@@ -106,6 +106,12 @@ hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_
                              const uint32_t* const* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st);
 // batches up to this size take the latency path (env PBFTV_WAVE_MAX overrides; 0 disables)
 uint64_t wave_path_max();
+// The latency path's result bytes (okbytes): bit 0 = the verdict; the
+// launched row kernel (k_ecdsa_rows) sets kRowsExact when the signature took
+// its exact rerun (a doubling or cancellation in the row tree, a live window
+// with two zero digits, r + n < p); the armed row kernel writes 2 instead
+// (the host reruns the certificate with a launch).  Counted by pbftv_qc_counters.
+constexpr int kRowsExact = 4;
 
 // The latency path's mailbox in pinned coherent host memory: a 64-B header,
 // then the inputs of up to cap signatures (hashes cap*32, r||s cap*64, key

@@ -214,12 +214,16 @@ struct Device {
   // the armed latency kernel (k_ecdsa_wave_armed): a persistent server that
   // waits for the next request's doorbell in `stage`; arm_seq = the request
   // number it waits for (0: none armed)
-  uint32_t arm_seq = 0, seq_counter = 0;  // (the armed kernel serves arm_seq, arm_seq + 1, ...)
+  // (arm_seq is written under d.mu; latency_device reads other devices' without their locks)
+  std::atomic<uint32_t> arm_seq{0};
+  uint32_t seq_counter = 0;                // (the armed kernel serves arm_seq, arm_seq + 1, ...)
   int arm_stream = 1;                      // qstream index of the armed kernel
   uint32_t armed_first = 0;                // the armed kernel's first number (its `live` report)
   uint32_t retiring = 0;                   // a rotated-out kernel still waiting for arm_seq's to start
-  uint32_t arm_waves = 0;                  // signatures the armed kernel serves: its slots (narrow) or kQcCap (wide)
+  uint32_t arm_waves = 0;                  // signatures the armed kernel serves: its slots (narrow) or workgroups (wide)
+  bool arm_wide = false;                   // the armed kernel is the wide one (helpers fed by the relay)
   uint32_t qc_nmax = 0;                    // largest narrow certificate since the last arming
+  uint32_t qc_nmax_prev = 0;               // ... and in the period before (slots shrink only after two)
   uint32_t qc_slots = 4;                   // slots the next narrow arming takes (the row schedule: a CU each)
   uint32_t qc_wmax = 0;                    // largest wide certificate (9..kQcCap) since the last arming
   uint32_t qc_wslots = 0;                  // workgroups of the wide arming (grows while wide is wanted; 0: none yet)
@@ -229,6 +233,8 @@ struct Device {
   // diagnostics of the last latency-path call (pbftv_qc_stamps)
   uint64_t qc_ns_entry = 0, qc_ns_handover = 0, qc_ns_total = 0, qc_ns_slots = 0;
   char hot_end[1] = {};
+  // counters of the latency path since the context opened (pbftv_qc_counters)
+  uint64_t qc_calls = 0, qc_armed = 0, qc_reruns = 0, qc_exact_sigs = 0, qc_launches = 0, qc_armings = 0;
   // when the lane-path batches enqueued so far are expected to finish
   // (steady-clock ns; an estimate from their sizes, kept without a HIP call):
   // a multi-device context sends a certificate to its least-loaded device
@@ -427,6 +433,25 @@ bool qc_yield() {
   return e && e[0] == '1';
 }
 
+// PBFTV_QC_SLOTS=k (1..kQcSlots): every narrow arming takes k slots; 0: unset
+uint32_t qc_slots_fixed() {
+  const char* e = getenv("PBFTV_QC_SLOTS");
+  const int k = e ? atoi(e) : 0;
+  return k >= 1 && k <= (int)QcMail::kQcSlots ? (uint32_t)k : 0u;
+}
+
+// per-certificate diagnostics on stderr (why a call was launched, a server
+// that left unserved, the 2-s timeout): PBFTV_TRACE_QC=1, a switch of its own
+// (PBFTV_TRACE, which bench.py sets for the registration phases, must not put
+// stderr writes on the latency path)
+bool trace_qc_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PBFTV_TRACE_QC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 int64_t steady_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
@@ -583,12 +608,17 @@ hipError_t qc_arm(Device& d) {
   // call came), at least 4 (a 3-vote certificate of a 4-replica committee, the
   // reference's default, and its 4-vote form); a larger one is served by a
   // launch and re-arms wider at once.  PBFTV_QC_SLOTS=k fixes k (1..8).
-  if (d.qc_nmax) d.qc_slots = std::max<uint32_t>(4, d.qc_nmax);
+  // (the largest of the last two periods with calls: mixed sizes, say 7- and
+  // 3-vote certificates, keep the wider arming instead of falling back to a
+  // launch after every half-budget rotation)
+  if (d.qc_nmax) {
+    d.qc_slots = std::max({4u, d.qc_nmax, d.qc_nmax_prev});
+    d.qc_nmax_prev = d.qc_nmax;
+  }
   d.qc_nmax = 0;
   const char* re = getenv("PBFTV_QC_ROWS");
-  const char* ke = getenv("PBFTV_QC_SLOTS");
   uint32_t slots = (re && re[0] == '0') ? QcMail::kQcSlots : d.qc_slots;
-  if (ke && atoi(ke) >= 1 && atoi(ke) <= (int)QcMail::kQcSlots) slots = (uint32_t)atoi(ke);
+  if (const uint32_t k = qc_slots_fixed()) slots = k;
   // wide: one workgroup per signature of the largest certificate seen while
   // wide ones keep coming, rounded up to 8 (a 67-vote certificate arms 72, not
   // 128 -- the resident footprint is ~6 waves per workgroup); a larger one is
@@ -619,7 +649,9 @@ hipError_t qc_arm(Device& d) {
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = d.armed_first = want;
   d.arm_waves = relay ? wslots : slots;
+  d.arm_wide = relay != nullptr;
   d.arm_live = false;
+  ++d.qc_armings;
   d.arm_stream = slot;
   d.armed_at = std::chrono::steady_clock::now();
   if (!d.keeper.joinable() && qc_keep_ms() > 0) d.keeper = std::thread(qc_keeper_loop, &d);
@@ -643,7 +675,7 @@ hipError_t qc_rotate(Device& d) {
   if (old) {
     if (d.retiring) __atomic_store_n(&qc_mail(d)->stop, d.retiring, __ATOMIC_RELEASE);  // (not live yet: rare)
     d.retiring = old;
-    if (d.arm_waves > QcMail::kQcSlots) {
+    if (d.arm_wide) {
       // a wide successor (up to 128 workgroups of ~6 waves) may not find room
       // beside its predecessor -- and beside other contexts' servers -- so
       // the predecessor leaves at once instead of overlapping (a wide
@@ -699,7 +731,9 @@ void qc_keeper_loop(Device* d) {
       wake = now + std::chrono::nanoseconds(busy_ns + 50000);
     } else if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
       // also re-arms after a disarm (key change) or a halt (quiesce)
-      const bool reshape = d->arm_seq && (d->arm_waves == kQcCap) != qc_wide_wanted(*d);
+      // (the kernel's SHAPE, narrow or wide, not its size: a wide arming takes
+      // as many workgroups as the largest recent wide certificate)
+      const bool reshape = d->arm_seq && d->arm_wide != qc_wide_wanted(*d);
       const bool left = d->arm_seq && __atomic_load_n(qc_mail(*d)->expired(d->arm_stream), __ATOMIC_ACQUIRE) == d->arm_seq;
       if (d->arm_seq == 0 || now >= d->armed_at + half || reshape || left) {  // (left: halted by a quiesce)
         if (qc_rotate(*d) != hipSuccess) (void)hipGetLastError();  // a call will launch instead
@@ -1620,7 +1654,8 @@ static Device* latency_device(pbftv_ctx* ctx) {
   if (best_free <= now) return best;
   for (auto& dp : ctx->devs) {
     const int64_t f = std::max<int64_t>(dp->busy_until_ns.load(std::memory_order_relaxed), now);
-    if (f < best_free || (f == best_free && f <= now && dp->arm_seq && !best->arm_seq)) {
+    if (f < best_free || (f == best_free && f <= now && dp->arm_seq.load(std::memory_order_relaxed) &&
+                          !best->arm_seq.load(std::memory_order_relaxed))) {
       best = dp.get();
       best_free = f;
     }
@@ -1855,7 +1890,9 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     std::memset(const_cast<uint8_t*>(res), 0xFF, n);
     m->cap = cap;
     m->n = (uint32_t)n;
+    ++d.qc_calls;
     auto launch_plain = [&]() -> int {
+      ++d.qc_launches;
       uint8_t* const hp = st8 + QcMail::hashes_off(cap);
       uint8_t* const sp = st8 + QcMail::sigs_off(cap);
       uint32_t* const kp = reinterpret_cast<uint32_t*>(st8 + QcMail::keys_off(cap));
@@ -1878,18 +1915,18 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       HIP_TRY(qc_disarm(d));
       collected = true;
     }
-    static const bool trace_qc = getenv("PBFTV_TRACE") != nullptr;
+    const bool trace_qc = trace_qc_enabled();
     if (trace_qc && small && d.arm_seq && n <= d.arm_waves && n > QcMail::kQcSlots && !qc_all_live(d)) {
       const uint32_t* lv = reinterpret_cast<const uint32_t*>(d.stage.as<uint8_t>() + QcMail::live_off(d.arm_stream));
       uint32_t k = 0;
       for (uint32_t w = 0; w < d.arm_waves; ++w) k += __atomic_load_n(lv + w, __ATOMIC_ACQUIRE) == d.armed_first;
       fprintf(stderr, "pbftv[dev %d] qc n=%llu launched: %u of %u workgroups of armed %u live (armed %.1f ms ago, retiring %u)\n",
-              d.id, (unsigned long long)n, k, d.arm_waves, d.arm_seq,
+              d.id, (unsigned long long)n, k, d.arm_waves, d.arm_seq.load(),
               std::chrono::duration<double, std::milli>(h_in - d.armed_at).count(), d.retiring);
     }
     if (trace_qc && small && !(d.arm_seq && n <= d.arm_waves))  // (diagnostics: why a launch)
       fprintf(stderr, "pbftv[dev %d] qc n=%llu launched: arm_seq=%u arm_waves=%u collected=%d wide_wanted=%d retiring=%u\n",
-              d.id, (unsigned long long)n, d.arm_seq, d.arm_waves, (int)collected, (int)qc_wide_wanted(d), d.retiring);
+              d.id, (unsigned long long)n, d.arm_seq.load(), d.arm_waves, (int)collected, (int)qc_wide_wanted(d), d.retiring);
     uint32_t cur = 0;  // the armed request number serving this call
     if (n > QcMail::kQcSlots && small) d.last_wide = h_in;
     if (n <= QcMail::kQcSlots) d.qc_nmax = std::max(d.qc_nmax, (uint32_t)n);
@@ -1937,8 +1974,11 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       int rc = launch_plain();
       if (rc != PBFTV_OK) return rc;
       if (small) {
-        if (d.arm_seq && n > d.arm_waves && (qc_wide_wanted(d) || n <= QcMail::kQcSlots))
-          HIP_TRY(qc_rotate(d));  // wide, or more slots (qc_nmax / qc_wmax), for the next one
+        // wide, or more slots (qc_nmax / qc_wmax), for the next one -- unless
+        // PBFTV_QC_SLOTS fixes the narrow shape, which would re-arm the same
+        const bool narrow_fixed = n <= QcMail::kQcSlots && qc_slots_fixed() && !qc_wide_wanted(d);
+        if (d.arm_seq && n > d.arm_waves && (qc_wide_wanted(d) || n <= QcMail::kQcSlots) && !narrow_fixed)
+          HIP_TRY(qc_rotate(d));
         HIP_TRY(qc_arm(d));  // the next call's server (no-op while one is armed)
       }
     }
@@ -2007,6 +2047,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       bool rerun = false;
       for (uint64_t i = 0; i < n; ++i) rerun |= res[i] == 2;
       if (rerun) {
+        ++d.qc_reruns;
         std::memset(const_cast<uint8_t*>(res), 0xFF, n);
         int rc = launch_plain();
         if (rc != PBFTV_OK) return rc;
@@ -2027,7 +2068,12 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       HIP_TRY(qc_disarm(d));
     }
     std::memset(out_bitmap, 0, (n + 7) / 8);
-    for (uint64_t i = 0; i < n; ++i) out_bitmap[i >> 3] |= (uint8_t)((res[i] & 1u) << (i & 7));
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint8_t b = res[i];
+      out_bitmap[i >> 3] |= (uint8_t)((b & 1u) << (i & 7));
+      d.qc_exact_sigs += (b & pbftv::kRowsExact) ? 1u : 0u;  // a launched row kernel's exact path
+    }
+    d.qc_armed += cur != 0;
     const auto h_out = std::chrono::steady_clock::now();
     auto ns = [](std::chrono::steady_clock::duration x) {
       return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(x).count();
@@ -2064,6 +2110,21 @@ int pbftv_qc_stamps(pbftv_ctx* ctx, int dev, uint64_t out[8]) {
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d->id);
   out[7] = (uint64_t)khz;
+  return PBFTV_OK;
+}
+
+int pbftv_qc_counters(pbftv_ctx* ctx, int dev, uint64_t out[8]) {
+  Device* d = dev_of(ctx, dev);
+  if (!d || !out) return fail(PBFTV_EINVAL, "bad context, device index or out pointer");
+  std::lock_guard<std::mutex> lk(d->mu);
+  out[0] = d->qc_calls;
+  out[1] = d->qc_armed;
+  out[2] = d->qc_reruns;
+  out[3] = d->qc_exact_sigs;
+  out[4] = d->qc_launches;
+  out[5] = d->qc_armings;
+  out[6] = d->rotations;
+  out[7] = d->arm_seq ? (uint64_t)d->arm_waves | ((uint64_t)(d->arm_wide ? 1 : 0) << 32) : 0;
   return PBFTV_OK;
 }
 

@@ -1221,9 +1221,10 @@ __device__ __forceinline__ void row_entry(const uint4* __restrict__ tab, int win
 }
 
 // kExact: the exceptional cases run wave 0's exact rerun here (the launched
-// kernel); without it (the armed kernel, which then needs far fewer registers
-// while it stays resident) they return 2 and the host serves the certificate
-// with the launched kernel.  Returns 1 / 0 (valid / not), or 2.
+// kernel) and the verdict carries kRowsExact; without it (the armed kernel,
+// which then needs far fewer registers while it stays resident) they return 2
+// and the host serves the certificate with the launched kernel.  Returns
+// 1 / 0 (valid / not), | kRowsExact (kernels.h) after the exact path, or 2.
 template <int WG, int WQ, bool kExact>
 __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint32_t r[8], const uint32_t s[8],
                                                  bool key_ok, const uint4* __restrict__ gtab,
@@ -1261,7 +1262,7 @@ __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint
       jac P;
       bool inf;
       wave_sum_lanes<WG, WQ>(P, inf, u1, u2, gtab, qt);
-      return ecdsa_check(P, !inf, r) ? 1 : 0;
+      return (ecdsa_check(P, !inf, r) ? 1 : 0) | kRowsExact;
     } else {
       return 2;
     }
@@ -1370,7 +1371,7 @@ __device__ __forceinline__ int block_verify_rows(const uint32_t e[8], const uint
       jac R;
       bool inf;
       wave_sum_lanes<WG, WQ>(R, inf, u1, u2, gtab, qt);
-      ok = ecdsa_check(R, !inf, r);
+      return (ecdsa_check(R, !inf, r) ? 1 : 0) | kRowsExact;
     } else {
       return 2;
     }
@@ -1410,9 +1411,9 @@ __device__ __forceinline__ bool wave_verify_sig(const uint8_t* __restrict__ hash
 }
 
 __device__ __forceinline__ void wave_store_verdict(bool ok, uint64_t i, uint64_t n, uint8_t* __restrict__ bitmap,
-                                                   uint8_t* __restrict__ okbytes) {
-  if (okbytes) {
-    okbytes[i] = ok ? 1 : 0;
+                                                   uint8_t* __restrict__ okbytes, uint8_t flags = 0) {
+  if (okbytes) {  // (the latency path's result bytes: bit 0 the verdict, kRowsExact the exact path)
+    okbytes[i] = (uint8_t)((ok ? 1 : 0) | flags);
     return;
   }
   // one bit of the LSB-first bitmap: set or clear it with a word atomic
@@ -1457,8 +1458,8 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows(const uint8_t* __
   bool key_ok = false;
   const uint4* qtab = nullptr;
   if (threadIdx.x < 64) wave_load_sig(hashes, sigs, key_idx, i, key_valid, nkeys, qtabs, e, r, s, key_ok, qtab);
-  const bool ok = block_verify_rows<WG, WQ, true>(e, r, s, key_ok, gtab, qtab, &sh) == 1;
-  if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
+  const int v = block_verify_rows<WG, WQ, true>(e, r, s, key_ok, gtab, qtab, &sh);
+  if (threadIdx.x == 0) wave_store_verdict((v & 1) != 0, i, n, bitmap, okbytes, (uint8_t)(v & kRowsExact));
 }
 
 // ---- the armed latency kernel ------------------------------------------------
@@ -1802,10 +1803,10 @@ void launch_armed_w(const ArmArgs& a, hipStream_t st) {
   // Whole CUs for the armed waves (opt-in, PBFTV_QC_EXCLUSIVE_CU, read at
   // every arming): an armed workgroup that takes its CU's whole LDS shares no
   // CU -- and no SIMD issue slots -- with a concurrent batch's blocks.
-  // "narrow": the 8-wave kernel only (2 CUs); "1": the 128-wave kernel too
-  // (32 CUs).  Off by default: with PBFTV_QC_YIELD (the default) no armed
-  // kernel is resident beside a batch, and beside one a whole CU costs the
-  // batch ~3 % (each XCD's share waits for its slowest CU).
+  // "narrow": the narrow kernel only (one CU per armed slot, up to 8); "1":
+  // the wide kernel too (one CU per workgroup, up to 128 CUs).  Off by
+  // default, as is PBFTV_QC_YIELD: a whole CU taken from a concurrent batch
+  // costs it 3-7 % (each XCD's share waits for its slowest CU).
   const char* e = getenv("PBFTV_QC_EXCLUSIVE_CU");
   const bool wide = a.relay != nullptr;
   const bool excl = e && (e[0] == '1' || (!wide && e[0] == 'n'));

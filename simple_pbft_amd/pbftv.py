@@ -75,6 +75,7 @@ def lib() -> ctypes.CDLL:
         "pbftv_qc_stamps": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
         "pbftv_set_latency_path_max": (ctypes.c_int, [_vp, ctypes.c_uint64]),
         "pbftv_qc_stamps_all": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_uint32]),
+        "pbftv_qc_counters": (ctypes.c_int, [_vp, ctypes.c_int, _vp]),
         "pbftv_hash_hex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_char_p]),
         "pbftv_sha256_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
         "pbftv_digest_check_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
@@ -569,6 +570,20 @@ class Verifier:
         o = np.zeros((n, 4), np.uint64)
         self._L.pbftv_qc_stamps_all(self._h, dev, o.ctypes.data, n)
         return o
+
+    def qc_counters(self, dev: int = 0) -> dict:
+        """pbftv_qc_counters: the latency path's counters since the context
+        opened -- calls, served armed, armed calls rerun by a launch (an
+        exceptional signature), signatures through a launched kernel's exact
+        path, launches, armings, keeper rotations -- and the armed kernel now
+        (armed_waves 0: none; armed_wide)."""
+        o = np.zeros(8, np.uint64)
+        _check(self._L.pbftv_qc_counters(self._h, dev, o.ctypes.data))
+        names = ("calls", "armed", "reruns", "exact_sigs", "launches", "armings", "rotations")
+        r = {k: int(v) for k, v in zip(names, o[:7])}
+        r["armed_waves"] = int(o[7]) & 0xFFFFFFFF
+        r["armed_wide"] = bool(int(o[7]) >> 32)
+        return r
 
     def qc_stamps(self, dev: int = 0) -> dict:
         """pbftv_qc_stamps: where the last latency-path call's time went (host

@@ -126,6 +126,23 @@ def test_bench_gpus_flag_starts_that_many_ranks(gpus):
     assert line["spawned"] == (gpus > 1) and line["shared_data"] == (gpus > 1)
 
 
+@pytest.mark.parametrize("stub", ["raise", "devices", "check", "ok"])
+def test_bench_in_context_failure_fails_the_run(stub):
+    """A failure of the one-process multi-device leg (an exception, a context
+    that does not span --gpus devices, a wrong bitmap) makes `bench.py --gpus N`
+    exit non-zero, with the line still printed.  The same
+    judgement (bench.in_context_result) as the real leg, on a stub leg."""
+    import json
+    r = _bench(["--gpus", "2", "--n", "4096"], {"PBFTV_BENCH_PROBE": f"in_context:{stub}"})
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    if stub == "ok":
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert line["in_context"]["devices"] == [0, 1]
+    else:
+        assert r.returncode != 0
+        assert "bench.py: in_context" in r.stderr
+
+
 def test_bench_gpus_mismatch_fails_loudly():
     """Under torch.distributed.run with a world size other than --gpus, bench.py refuses."""
     r = _bench(["--gpus", "2", "--n", "4096"], {"WORLD_SIZE": "1"})

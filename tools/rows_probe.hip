@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) rows_probe_k(const uint8_t* __
   bool key_ok = false;
   const uint4* qtab = nullptr;
   if (threadIdx.x < 64) wave_load_sig(hashes, sigs, key_idx, i, key_valid, nkeys, qtabs, e, r, s, key_ok, qtab);
-  const bool ok = block_verify_rows<WG, WQ, true>(e, r, s, key_ok, gtab, qtab, &sh) == 1;
+  const bool ok = block_verify_rows<WG, WQ, true>(e, r, s, key_ok, gtab, qtab, &sh) & 1;
   if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, nullptr);
 }
 
