@@ -422,6 +422,69 @@ def qc_driver():
     return _QC_DRIVER
 
 
+# the reference's own 99-byte request preimage (log/node1.log:3, tests/golden/digest_kats.json)
+REQUEST_PREIMAGE = (b'{"timestamp":1668519246,"clientID":"client1","operation":"printf",'
+                    b'"sequenceID":1668519247222762700}')
+
+
+def single_calls(ver: Verifier, reps: int = 2000) -> dict:
+    """The single-call drop-ins, each called from C (tools/qc_driver.c) as a
+    cgo caller would, p50 / p99 over reps back-to-back calls (VERDICT r5 item
+    7), beside the same single call on the CPU:
+      hash_hex:    pbftv_hash_hex (utils.Hash, utils/utils.go:13-17) on the
+                   99-byte request preimage -- the reference hashes once per
+                   request at pbft_impl.go:73 (StartConsensus) and re-hashes
+                   the request for every vote in verifyMsg (:190);
+      verify_msg:  pbftv_verify_msg_batch at n = 1 (verifyMsg's compare, host code);
+      verify_1sig: a 1-signature pbftv_qc_verify (the armed latency kernel);
+    and OpenSSL's EVP_Digest + hex (oracle/openssl_standin.c), a 1-signature
+    ECDSA_do_verify on one thread."""
+    D = qc_driver()
+    vp = ctypes.c_void_p
+    D.hash_drive.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_char_p]
+    D.vmsg_drive.argtypes = [vp, vp, ctypes.c_char_p, ctypes.c_uint32, vp]
+    L = lib_handle(ver)
+    msg = np.frombuffer(REQUEST_PREIMAGE, np.uint8)
+    import hashlib
+    want = hashlib.sha256(REQUEST_PREIMAGE).hexdigest()
+
+    def pct(us):
+        return {"p50": float(np.percentile(us, 50)), "p99": float(np.percentile(us, 99)), "min": float(us.min()),
+                "calls": len(us)}
+    out = {"message_bytes": len(REQUEST_PREIMAGE)}
+    us = np.zeros(reps)
+    hx = ctypes.create_string_buffer(65)
+    D.hash_drive(ctypes.cast(L.pbftv_hash_hex, vp).value, ver.handle.value, msg.ctypes.data, len(msg), 50,
+                 us.ctypes.data, hx)  # (warm)
+    bad = D.hash_drive(ctypes.cast(L.pbftv_hash_hex, vp).value, ver.handle.value, msg.ctypes.data, len(msg), reps,
+                       us.ctypes.data, hx)
+    out["hash_hex"] = {**pct(us), "ok": bad == 0 and hx.value.decode() == want}
+    dg = np.frombuffer(bytes.fromhex(want), np.uint8).copy()
+    bad = D.vmsg_drive(ctypes.cast(L.pbftv_verify_msg_batch, vp).value, dg.ctypes.data, want.encode(), reps,
+                       us.ctypes.data)
+    out["verify_msg"] = {**pct(us), "ok": bad == 0}
+    q1 = qc_latency(ver, 4, 1, reps, 17)
+    out["verify_1sig"] = {k: q1[k] for k in ("p50", "p99", "min", "calls", "armed_frac")}
+    so = os.path.join(ROOT, "oracle", "libopenssl_standin.so")
+    if os.path.exists(so):
+        S = ctypes.CDLL(so)
+        S.standin_hash_hex_drive.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_char_p]
+        S.standin_hash_hex_drive(msg.ctypes.data, len(msg), 50, us.ctypes.data, hx)
+        bad = S.standin_hash_hex_drive(msg.ctypes.data, len(msg), reps, us.ctypes.data, hx)
+        out["cpu_hash_hex"] = {**pct(us), "ok": bad == 0 and hx.value.decode() == want,
+                               "kind": "openssl_standin EVP_Digest, caller's thread"}
+        S.standin_qc_latency.restype = ctypes.c_int64
+        S.standin_qc_latency.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint32,
+                                         ctypes.c_int, ctypes.c_double, vp, vp]
+        pub, H, S1, K = synth.certs(4, 1, 400, 18)
+        us1 = np.zeros(400)
+        bm = np.zeros(64, np.uint8)
+        acc = S.standin_qc_latency(H.ctypes.data, S1.ctypes.data, K.ctypes.data, 400, 1, pub.ctypes.data, len(pub),
+                                   1, 0.0, us1.ctypes.data, bm.ctypes.data)
+        out["cpu_verify_1sig"] = {**pct(us1), "ok": acc == 400, "kind": "openssl_standin ECDSA_do_verify, 1 thread"}
+    return out
+
+
 def qc_latency(ver: Verifier, n_keys: int, sigs: int, iters: int, seed: int, gap_s: float = 0.0, warm: int = 20,
                register: bool = True, certs=None):
     """Latency of pbftv_qc_verify on one certificate from host buffers: every
@@ -1250,6 +1313,8 @@ def main():
                               "pbft/network/node.go:44)",
                 "detail": {"n4": q4, "n4_tick": q4_tick, "n4_gap100ms": q4_100, "n100": q100, "n100_tick": q100_tick},
                 "under_load": load}
+            # the single-call drop-ins beside their CPU counterparts
+            out["single_calls_us"] = single_calls(ver)
             # the CPU baseline on every host CPU this process may use (affinity
             # mask capped by the cgroup quota, with the evidence), plus the
             # 16-thread figure of the box's nominal per-GPU share as a labelled extra

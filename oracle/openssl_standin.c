@@ -300,3 +300,24 @@ int standin_sha256_batch(const uint8_t* data, const uint64_t* offsets, const uin
   free(jobs);
   return 0;
 }
+
+/* utils.Hash of ONE message on the caller's thread (EVP_Digest SHA-256 +
+ * lowercase hex), reps calls, out_us[i] each call's wall time: the CPU side
+ * of bench.py single_calls_us. */
+int standin_hash_hex_drive(const uint8_t* msg, uint64_t len, uint32_t reps, double* out_us, char out_hex[65]) {
+  static const char hx[] = "0123456789abcdef";
+  unsigned char d[32];
+  unsigned int dl = 0;
+  int bad = 0;
+  for (uint32_t i = 0; i < reps; ++i) {
+    const double t0 = now_us();
+    bad += EVP_Digest(msg, len, d, &dl, EVP_sha256(), NULL) != 1;
+    for (int k = 0; k < 32; ++k) {
+      out_hex[2 * k] = hx[d[k] >> 4];
+      out_hex[2 * k + 1] = hx[d[k] & 15];
+    }
+    out_hex[64] = 0;
+    out_us[i] = now_us() - t0;
+  }
+  return bad;
+}

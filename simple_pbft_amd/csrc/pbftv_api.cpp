@@ -20,6 +20,7 @@
 #include <functional>
 #include <initializer_list>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -278,6 +279,15 @@ struct Device {
   // pinned staging for the one H2D and the results
   DevBuf arena, msgok;
   HostBuf mstage, mout;
+  HostBuf sstage;  // zero-copy inputs/digests of small digest calls (sha_host_small)
+  // pbftv_dev_alloc / pbftv_dev_free: a stream-ordered pool of the library's
+  // own (allocations on astream, frees on fstream behind every stream of the
+  // context), so a caller's free neither synchronises the GPU nor halts the
+  // armed servers (dev_pool_free)
+  hipMemPool_t pool = nullptr;
+  hipStream_t astream = nullptr, fstream = nullptr;
+  std::set<void*> pool_ptrs;
+  std::vector<hipEvent_t> fence_ev;
   // Device scratch (rec, prefix, ksort, okb, order_scratch) is shared by
   // calls on d.stream and on caller streams (the *_dev entry points).  The
   // mutex orders the enqueues; this event orders the execution: a call on a
@@ -780,6 +790,15 @@ struct pbftv_ctx {
   // a certificate ~3 us after an idle second)
   std::atomic<uint64_t> wave_max{2048};
   Device* dev0 = nullptr;  // devs[0], one hop less for the latency path's first (cold) loads
+  // pbftv_host_alloc / pbftv_host_free: freed pinned blocks are kept for
+  // reuse (hipHostFree waits for every kernel on every GPU, so a free would
+  // halt the armed servers); released at close, or when the cache passes
+  // kHostCacheBytes (then under a quiesce)
+  std::mutex host_mu;
+  std::map<void*, size_t> host_live;          // block -> its size
+  std::multimap<size_t, void*> host_cache;    // size -> free block
+  size_t host_cache_bytes = 0;
+  static constexpr size_t kHostCacheBytes = size_t(1) << 30;
 };
 
 namespace {
@@ -1052,7 +1071,7 @@ void pbftv_close(pbftv_ctx* ctx) {
                       &d->bitmap, &d->data, &d->offsets, &d->lengths, &d->order,
                       &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok})
       b->release();  // explicit, with this device current (the destructors are a backstop)
-    for (HostBuf* b : {&d->stage, &d->mstage, &d->mout}) b->release();
+    for (HostBuf* b : {&d->stage, &d->mstage, &d->mout, &d->sstage}) b->release();
     if (d->scratch_ev) (void)hipEventDestroy(d->scratch_ev);
     for (auto& kv : d->reader_ev) (void)hipEventDestroy(kv.second);
     d->reader_ev.clear();
@@ -1081,7 +1100,22 @@ void pbftv_close(pbftv_ctx* ctx) {
       if (d->h2d_ev[k]) (void)hipEventDestroy(d->h2d_ev[k]);
       if (d->comp_ev[k]) (void)hipEventDestroy(d->comp_ev[k]);
     }
+    if (d->pool) {  // blocks the caller did not free go with the context
+      GpuQuiesce quiet(d->id);
+      for (void* p : d->pool_ptrs) (void)hipFreeAsync(p, d->fstream);
+      d->pool_ptrs.clear();
+      (void)hipStreamSynchronize(d->fstream);
+      (void)hipStreamSynchronize(d->astream);
+      (void)hipMemPoolDestroy(d->pool);
+      (void)hipStreamDestroy(d->fstream);
+      (void)hipStreamDestroy(d->astream);
+    }
+    for (hipEvent_t e : d->fence_ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
+  }
+  if (!ctx->host_cache.empty()) {
+    GpuQuiesce quiet(-1);
+    for (auto& kv : ctx->host_cache) (void)hipHostFree(kv.second);
   }
   delete ctx;
 }
@@ -1115,26 +1149,113 @@ static Device* dev_of(pbftv_ctx* ctx, int dev) {
   return ctx->devs[dev].get();
 }
 
+// The device pool of pbftv_dev_alloc: memory is never returned to the
+// driver while the context lives (release threshold: unlimited), so a free
+// is a stream-ordered bookkeeping step, not hipFree (which waits for every
+// kernel on the GPU, the armed servers included).  Allocations are made on
+// astream and reuse only blocks whose free has completed (no reuse that would
+// make an allocation wait for a pending free); frees go on fstream.
+static hipError_t dev_pool_ready(Device& d) {
+  if (d.pool) return hipSuccess;
+  hipMemPoolProps props{};
+  props.allocType = hipMemAllocationTypePinned;
+  props.handleTypes = hipMemHandleTypeNone;
+  props.location.type = hipMemLocationTypeDevice;
+  props.location.id = d.id;
+  HIP_TRY_E(hipMemPoolCreate(&d.pool, &props));
+  uint64_t keep = UINT64_MAX;
+  HIP_TRY_E(hipMemPoolSetAttribute(d.pool, hipMemPoolAttrReleaseThreshold, &keep));
+  int no = 0;
+  HIP_TRY_E(hipMemPoolSetAttribute(d.pool, hipMemPoolReuseAllowInternalDependencies, &no));
+  HIP_TRY_E(hipMemPoolSetAttribute(d.pool, hipMemPoolReuseFollowEventDependencies, &no));
+  HIP_TRY_E(hipStreamCreateWithFlags(&d.astream, hipStreamNonBlocking));
+  HIP_TRY_E(hipStreamCreateWithFlags(&d.fstream, hipStreamNonBlocking));
+  return hipSuccess;
+}
+
+// fstream waits, on the GPU, for everything the context may still run on a
+// buffer: its own streams, its library streams and every caller stream it
+// was given (the scratch fence and the reader fences) -- no host wait.
+static hipError_t fence_free_stream(Device& d) {
+  std::vector<hipStream_t> sts;
+  for (hipStream_t s : {d.stream, d.stream2, d.cstream, d.lstream})
+    if (s) sts.push_back(s);
+  for (auto& kv : d.stream_scratch) sts.push_back(kv.first);
+  while (d.fence_ev.size() < sts.size()) {
+    hipEvent_t e;
+    HIP_TRY_E(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    d.fence_ev.push_back(e);
+  }
+  for (size_t i = 0; i < sts.size(); ++i) {
+    HIP_TRY_E(hipEventRecord(d.fence_ev[i], sts[i]));
+    HIP_TRY_E(hipStreamWaitEvent(d.fstream, d.fence_ev[i], 0));
+  }
+  if (d.scratch_st && d.scratch_st != d.stream && d.scratch_ev)
+    HIP_TRY_E(hipStreamWaitEvent(d.fstream, d.scratch_ev, 0));
+  for (auto& kv : d.reader_ev) HIP_TRY_E(hipStreamWaitEvent(d.fstream, kv.second, 0));
+  return hipSuccess;
+}
+
 int pbftv_dev_alloc(pbftv_ctx* ctx, int dev, uint64_t bytes, void** out_ptr) {
   Device* d = dev_of(ctx, dev);
   if (!d || !out_ptr) return fail(PBFTV_EINVAL, "bad context, device index or out pointer");
+  std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
-  HIP_TRY(hipMalloc(out_ptr, bytes ? bytes : 1));
+  HIP_TRY(dev_pool_ready(*d));
+  HIP_TRY(hipMallocFromPoolAsync(out_ptr, bytes ? bytes : 1, d->pool, d->astream));
+  HIP_TRY(hipStreamSynchronize(d->astream));  // (usable on any stream once this returns)
+  d->pool_ptrs.insert(*out_ptr);
   return PBFTV_OK;
 }
 
 int pbftv_host_alloc(pbftv_ctx* ctx, uint64_t bytes, void** out_ptr) {
   if (!ctx || !out_ptr || ctx->devs.empty()) return fail(PBFTV_EINVAL, "bad context or out pointer");
+  const size_t want = bytes ? bytes : 1;
+  {
+    // a cached block of at least the size and at most twice it
+    std::lock_guard<std::mutex> lk(ctx->host_mu);
+    auto it = ctx->host_cache.lower_bound(want);
+    if (it != ctx->host_cache.end() && it->first <= 2 * want) {
+      *out_ptr = it->second;
+      ctx->host_live[it->second] = it->first;
+      ctx->host_cache_bytes -= it->first;
+      ctx->host_cache.erase(it);
+      return PBFTV_OK;
+    }
+  }
   HIP_TRY(hipSetDevice(ctx->devs[0]->id));
-  HIP_TRY(hipHostMalloc(out_ptr, bytes ? bytes : 1, hipHostMallocPortable));
+  HIP_TRY(hipHostMalloc(out_ptr, want, hipHostMallocPortable));
+  std::lock_guard<std::mutex> lk(ctx->host_mu);
+  ctx->host_live[*out_ptr] = want;
   return PBFTV_OK;
 }
 
 int pbftv_host_free(pbftv_ctx* ctx, void* ptr) {
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
-  if (ptr) {
+  if (!ptr) return PBFTV_OK;
+  std::vector<void*> evict;
+  {
+    std::lock_guard<std::mutex> lk(ctx->host_mu);
+    auto it = ctx->host_live.find(ptr);
+    if (it != ctx->host_live.end()) {
+      // kept for the next pbftv_host_alloc: no hipHostFree, so no GPU-wide
+      // wait and no halt of the armed servers
+      ctx->host_cache.emplace(it->second, ptr);
+      ctx->host_cache_bytes += it->second;
+      ctx->host_live.erase(it);
+      ptr = nullptr;
+      while (ctx->host_cache_bytes > pbftv_ctx::kHostCacheBytes) {  // the largest blocks go
+        auto big = std::prev(ctx->host_cache.end());
+        ctx->host_cache_bytes -= big->first;
+        evict.push_back(big->second);
+        ctx->host_cache.erase(big);
+      }
+    }
+  }
+  if (ptr) evict.push_back(ptr);  // (not ours: freed as before)
+  if (!evict.empty()) {
     GpuQuiesce quiet(-1);  // hipHostFree waits for every kernel: armed ones leave first
-    HIP_TRY(hipHostFree(ptr));
+    for (void* p : evict) HIP_TRY(hipHostFree(p));
   }
   return PBFTV_OK;
 }
@@ -1142,11 +1263,20 @@ int pbftv_host_free(pbftv_ctx* ctx, void* ptr) {
 int pbftv_dev_free(pbftv_ctx* ctx, int dev, void* ptr) {
   Device* d = dev_of(ctx, dev);
   if (!d) return fail(PBFTV_EINVAL, "bad context or device index");
+  if (!ptr) return PBFTV_OK;
+  std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
-  if (ptr) {
-    GpuQuiesce quiet(d->id);  // hipFree waits for every kernel on the GPU: armed ones leave first
-    HIP_TRY(hipFree(ptr));
+  auto it = d->pool_ptrs.find(ptr);
+  if (it != d->pool_ptrs.end()) {
+    // stream-ordered: the block returns to the pool once the context's work
+    // queued so far has passed (fstream waits for it on the GPU)
+    d->pool_ptrs.erase(it);
+    HIP_TRY(fence_free_stream(*d));
+    HIP_TRY(hipFreeAsync(ptr, d->fstream));
+    return PBFTV_OK;
   }
+  GpuQuiesce quiet(d->id);  // (not from the pool) hipFree waits for every kernel on the GPU: armed ones leave first
+  HIP_TRY(hipFree(ptr));
   return PBFTV_OK;
 }
 
@@ -2190,10 +2320,53 @@ int pbftv_sha256_batch_dev(pbftv_ctx* ctx, int dev, const uint8_t* d_data, const
   return PBFTV_OK;
 }
 
+// Small host-buffer digest calls (utils.Hash of one request, a handful of
+// messages): no DMA at all.  The messages, offsets and lengths are packed into
+// pinned device-coherent host memory that k_sha256 reads over the bus, the
+// digests (and match bits) come back the same way, and one launch on the
+// latency stream plus its synchronisation is the whole device part -- instead
+// of three copies up, the block-count sort, the kernel and a copy down
+// (pbftv_hash_hex 99 B: profiles/r06_single_calls.json).
+constexpr uint64_t kShaZeroCopyMsgs = 64, kShaZeroCopyBytes = 64 << 10;
+
+static int sha_host_small(Device& d, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
+                          uint64_t n, uint64_t lo_b, uint64_t span, uint8_t* out_digests) {
+  // layout: offsets (8n) | lengths (4n) | digests (32n) | data (span + 256: k_sha256 reads whole aligned lines)
+  const uint64_t o_len = 8 * n, o_dig = o_len + 4 * n;
+  const uint64_t o_data = (o_dig + 32 * n + 127) & ~127ull;
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIP_TRY(hipSetDevice(d.id));
+  HIP_TRY(d.sstage.ensure(o_data + span + 256));
+  uint8_t* b = d.sstage.as<uint8_t>();
+  uint64_t* off = reinterpret_cast<uint64_t*>(b);
+  for (uint64_t i = 0; i < n; ++i) off[i] = offsets[i] - lo_b;
+  std::memcpy(b + o_len, lengths, 4 * n);
+  if (span) std::memcpy(b + o_data, data + lo_b, span);
+  if (!d.lstream) HIP_TRY(hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking));
+  HIP_TRY(timed(d, PBFTV_K_SHA256, d.lstream, [&] {
+    return pbftv::launch_sha256(b + o_data, off, reinterpret_cast<const uint32_t*>(b + o_len), nullptr, n, b + o_dig,
+                                nullptr, nullptr, d.lstream);
+  }));
+  HIP_TRY(hipStreamSynchronize(d.lstream));
+  std::memcpy(out_digests, b + o_dig, 32 * n);
+  return PBFTV_OK;
+}
+
 static int sha_host(pbftv_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lengths,
                     const uint8_t* expected, uint64_t n, uint8_t* out_digests, uint8_t* out_bitmap) {
   if (!ctx) return fail(PBFTV_EINVAL, "ctx is null");
   if (n && (!offsets || !lengths)) return fail(PBFTV_EINVAL, "null buffer");
+  if (n && n <= kShaZeroCopyMsgs && !expected) {  // (match bits: device atomics, so the DMA path)
+    uint64_t lo_b = UINT64_MAX, hi_b = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      lo_b = std::min(lo_b, offsets[i]);
+      hi_b = std::max(hi_b, offsets[i] + lengths[i]);
+    }
+    if (lo_b > hi_b) lo_b = hi_b;
+    if (hi_b > lo_b && !data) return fail(PBFTV_EINVAL, "data is null");
+    if (hi_b - lo_b <= kShaZeroCopyBytes)
+      return sha_host_small(*ctx->dev0, data, offsets, lengths, n, lo_b, hi_b - lo_b, out_digests);
+  }
   return run_sharded(ctx, n, [&](Device& d, Shard s) -> int {
     const uint64_t m = s.hi - s.lo;
     // byte span of this shard, re-based offsets

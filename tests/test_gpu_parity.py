@@ -106,6 +106,32 @@ def test_digest_check(ver):
     assert (got == ~flip).all()
 
 
+def test_sha256_small_calls_zero_copy(ver):
+    """Digest calls of <= 64 messages and <= 64 KiB (pbftv_hash_hex, a few
+    requests) take the zero-copy path: the messages packed into pinned
+    coherent host memory that k_sha256 reads over the bus, digests written
+    back the same way, one launch.  Every size class, offsets at every byte
+    alignment, empty messages, the 64-message / 64-KiB limits and one past
+    each (the DMA path) against hashlib."""
+    rng = np.random.default_rng(23)
+    for n, maxlen in [(1, 0), (1, 1), (1, 55), (1, 56), (1, 64), (1, 99), (1, 4096), (1, 65536), (1, 65537),
+                      (2, 300), (7, 1000), (33, 130), (64, 1024), (64, 1025), (65, 200)]:
+        lens = rng.integers(0, maxlen + 1, n).astype(np.uint32)
+        lens[0] = maxlen
+        gaps = rng.integers(0, 9, n)
+        offs = np.zeros(n, np.uint64)
+        pos = int(rng.integers(0, 200))
+        for i in range(n):
+            offs[i] = pos
+            pos += int(lens[i]) + int(gaps[i])
+        data = np.frombuffer(rng.bytes(pos + 8), np.uint8).copy()
+        got = ver.sha256_batch(data, offs, lens)
+        want = [hashlib.sha256(data[int(o):int(o) + int(l)].tobytes()).digest() for o, l in zip(offs, lens)]
+        assert [g.tobytes() for g in got] == want, (n, maxlen)
+    for m in (b"", b"a", bytes(range(99)), rng.bytes(1 << 16)):
+        assert ver.hash_hex(m) == hashlib.sha256(m).hexdigest()
+
+
 def test_hash_hex_and_request_digests(ver, digest_kats):
     """utils.Hash / digest(*RequestMsg) on the reference's own logged requests."""
     reqs = []
@@ -621,13 +647,57 @@ def test_armed_slots_follow_certificate_size(oracle_lib, monkeypatch):
     assert not armed[8] and armed[9] and armed[10], served  # 8 > 7: once launched
 
 
+def test_wide_arming_is_kept_by_the_keeper(oracle_lib, monkeypatch):
+    """a wide arming takes as many workgroups as the
+    largest recent wide certificate (72 for 67 votes), and the keeper used to
+    compare that SIZE with 128 to decide whether to reshape -- so it rotated
+    a freshly armed wide server at once and on every wake.  The keeper now
+    compares the SHAPE.  Right after the call that armed the wide kernel, wide
+    certificates back to back are served by it (once all its workgroups are
+    resident) with no further arming or rotation; every bit vs the oracle."""
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", "4000")  # (no timed rotation within the test)
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=5, per_key=30, seed=93)
+    sigs[::6, 44] ^= 0x10
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    rng = np.random.default_rng(94)
+
+    def call(n):
+        o = rng.choice(n_all, n, replace=False)
+        assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all()
+        return v.qc_stamps(0)["armed"]
+
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        call(3)
+        call(3)
+        assert not call(67)  # launched; the call path arms the wide kernel
+        c0 = v.qc_counters(0)
+        assert c0["armed_wide"] and c0["armed_waves"] == 72, c0
+        t0 = time.monotonic()
+        while not call(67):  # launched until every workgroup is resident
+            assert time.monotonic() - t0 < 2.0, v.qc_counters(0)
+        time.sleep(0.02)     # the keeper has woken since
+        for _ in range(2):
+            assert call(67)
+        c1 = v.qc_counters(0)
+        assert (c1["armings"], c1["rotations"]) == (c0["armings"], c0["rotations"]), (c0, c1)
+        assert c1["armed_wide"] and c1["armed_waves"] == 72
+
+
 def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypatch):
     """An armed kernel with a 5-s budget stays resident between calls.  A
-    device free and a pinned-host free must not wait for it: the library
-    quiesces the GPU (halts every armed kernel on it) first.  Another
-    context's key change waits only for its OWN work (ctx_quiesce), so it does
-    not wait for context a's armed kernel either.  The halted context's next
-    call falls back to a launch and is still right."""
+    device free and a pinned-host free neither wait for it nor stop it
+    (VERDICT r5 item 6): pbftv_dev_alloc memory comes from a stream-ordered
+    pool and its free is queued behind the context's streams (no hipFree),
+    pinned blocks go back to a cache (no hipHostFree) -- so both contexts'
+    servers keep serving right after (pbftv_qc_counters).  Another context's
+    key change waits only for its OWN work (ctx_quiesce)."""
     import time
     from simple_pbft_amd import Verifier
     monkeypatch.setenv("PBFTV_QC_ARM_MS", "5000")
@@ -638,29 +708,40 @@ def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypa
     oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
                                               keys.ctypes.data, len(keys), want.ctypes.data, 8)
     want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+
+    def call(v, i):
+        assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all(), i
+        return v.qc_stamps(0)["armed"]
+
     with Verifier(device_mask=1) as a, Verifier(device_mask=1) as b:
         a.register_keys(keys)
         b.register_keys(keys)
         for v in (a, b):
             for i in range(0, 12, 3):
-                assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
-        buf = a.alloc(0, 1 << 20)
-        t0 = time.perf_counter()
-        buf.free()
-        assert time.perf_counter() - t0 < 0.5
-        pin = a.pinned(np.zeros(1 << 16, np.uint8))
-        t0 = time.perf_counter()
-        pin.free()
-        assert time.perf_counter() - t0 < 0.5
-        for i in range(12, 24, 3):  # both contexts re-armed (or launched) and right
-            assert (a.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
-            assert (b.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all()
+                call(v, i)
+            assert call(v, 0)
+        c0 = {id(v): v.qc_counters(0) for v in (a, b)}
+        for _ in range(20):
+            buf = a.alloc(0, 1 << 20)
+            t0 = time.perf_counter()
+            buf.free()
+            assert time.perf_counter() - t0 < 0.05
+            pin = a.pinned(np.zeros(1 << 16, np.uint8))
+            t0 = time.perf_counter()
+            pin.free()
+            assert time.perf_counter() - t0 < 0.05
+            for v in (a, b):  # served by the same armed servers, right after the frees
+                assert call(v, 12)
+        for v in (a, b):
+            c1 = v.qc_counters(0)
+            assert c1["armings"] == c0[id(v)]["armings"] and c1["armed"] - c0[id(v)]["armed"] == 20, (c0[id(v)], c1)
         t0 = time.perf_counter()
         assert b.set_key(1, keys[1])  # b's key change with a's kernel armed (b waits for b's work only)
         assert time.perf_counter() - t0 < 2.0
+        assert call(a, 15)  # (a's server was not stopped by it)
         for i in range(24, n_all - 3, 3):
             for v in (a, b):
-                assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all(), i
+                call(v, i)
 
 
 def test_armed_kernels_of_two_contexts_concurrent(oracle_lib):

@@ -119,6 +119,7 @@ def test_row_tree_exceptional_paths(gq, ecdsa_fixtures, monkeypatch):
         # (a) the armed narrow kernel, certificates of 4: two crafted (a
         # signature and its twin, or two of a kind) and two plain golden ones
         monkeypatch.setenv("PBFTV_QC_ARM", "1")
+        monkeypatch.setenv("PBFTV_QC_WIDE", "0")  # (phase (c)'s 128s would arm the wide kernel)
         _wait_armed(v, plain[:3], wide=False)
         for a in range(0, len(crafted), 2):
             rows = crafted[a:a + 2] + plain[(a % 40):(a % 40) + 2]
@@ -134,6 +135,7 @@ def test_row_tree_exceptional_paths(gq, ecdsa_fixtures, monkeypatch):
         # (b) the armed wide kernel: 67-signature certificates, crafted ones
         # at slot positions (< 8) and helper positions (>= 8)
         filler = (plain * 4)[:67]
+        monkeypatch.delenv("PBFTV_QC_WIDE")
         _wait_armed(v, filler, wide=True)  # (the first wide call is launched, the next arming is wide)
         per = 20
         for a in range(0, len(crafted), per):

@@ -1,0 +1,38 @@
+"""A bounded run of tools/stress.py inside the GPU suite:
+the standing check for the family of round 4's unexplained 0-of-67 false
+reject -- a key change, a free or a keeper rotation racing a certificate or a
+batch.  Two contexts on the GPU; worker threads submit certificates of 3 / 8 /
+67 / 129 signatures (armed narrow, armed wide, launched), host-buffer and
+device-resident lane batches, while a control thread switches a context's
+whole key set, re-sets a key and frees device / pinned memory every 0.2-0.6 s
+and the keepers rotate every 15 ms.  Every certificate carries corrupted
+votes and every bitmap is compared with the oracle's.  Its own process (the
+tool sets PBFTV_* for itself), ~40 s of racing."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_stress_races_every_answer_checked():
+    env = {k: v for k, v in os.environ.items() if not k.startswith("PBFTV_")}
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "stress.py"), "--seconds", "40"],
+                       env=env, capture_output=True, text=True, timeout=200)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert lines, (r.returncode, r.stderr[-3000:])
+    out = json.loads(lines[-1])
+    assert r.returncode == 0 and out["wrong"] == 0 and not out["errors"] and not out["hung_threads"], out
+    c = out["counts"]
+    # every kind of operation raced at least a few times
+    for k in ("cert3", "cert8", "cert67", "cert129", "host_batch", "dev_batch"):
+        assert c.get(k, 0) >= 5, c
+    assert c.get("ctl_switch", 0) + c.get("ctl_set_key", 0) >= 5 and c.get("ctl_dev_free", 0) >= 1, c
+    print(json.dumps({"stress": {"seconds": out["seconds"], "counts": c}}))

@@ -57,3 +57,39 @@ int qc_drive(void* verify, void* stamps, void* ctx, const uint8_t* hashes, const
   }
   return failed;
 }
+
+/* The single-call drop-ins, timed the same way (bench.py single_calls_us):
+ * pbftv_hash_hex (utils.Hash, utils/utils.go:13-17, called once per request
+ * at pbft_impl.go:73) on one message, reps calls, out_us[i] each call's wall
+ * time; out_hex = the last digest.  Returns the number of failed calls. */
+typedef int (*hash_hex_fn)(void* ctx, const uint8_t* content, uint64_t len, char out_hex[65]);
+int hash_drive(void* fn, void* ctx, const uint8_t* msg, uint64_t len, uint32_t reps, double* out_us, char* out_hex) {
+  hash_hex_fn h = (hash_hex_fn)fn;
+  int failed = 0;
+  for (uint32_t i = 0; i < reps; ++i) {
+    const double t0 = now_us();
+    failed += h(ctx, msg, len, out_hex) != 0;
+    out_us[i] = now_us() - t0;
+  }
+  return failed;
+}
+
+/* pbftv_verify_msg_batch at n = 1 (State.verifyMsg, pbft_impl.go:176-202, for
+ * one vote): host code, no device. */
+typedef int (*vmsg_fn)(int64_t view, int64_t last, const uint8_t* req_digest, uint64_t n, const int64_t* views,
+                       const int64_t* seqs, const char* got, const uint64_t* got_off, const uint32_t* got_len,
+                       uint8_t* out_bitmap);
+int vmsg_drive(void* fn, const uint8_t* req_digest, const char* hex64, uint32_t reps, double* out_us) {
+  vmsg_fn v = (vmsg_fn)fn;
+  int64_t view = 0, seq = 7;
+  uint64_t off = 0;
+  uint32_t len = 64;
+  uint8_t bm[8];
+  int bad = 0;
+  for (uint32_t i = 0; i < reps; ++i) {
+    const double t0 = now_us();
+    bad += v(0, 6, req_digest, 1, &view, &seq, hex64, &off, &len, bm) != 0 || (bm[0] & 1) != 1;
+    out_us[i] = now_us() - t0;
+  }
+  return bad;
+}
