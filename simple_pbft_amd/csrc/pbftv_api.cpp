@@ -281,13 +281,19 @@ struct Device {
   HostBuf mstage, mout;
   HostBuf sstage;  // zero-copy inputs/digests of small digest calls (sha_host_small)
   // pbftv_dev_alloc / pbftv_dev_free: a stream-ordered pool of the library's
-  // own (allocations on astream, frees on fstream behind every stream of the
-  // context), so a caller's free neither synchronises the GPU nor halts the
-  // armed servers (dev_pool_free)
+  // own, so a caller's free neither synchronises the GPU nor halts the armed
+  // servers.  A freed block waits in pending_frees until every stream of the
+  // context has passed the point where the free was called (events polled on
+  // the host, no stream waits on the GPU), then returns to the pool
+  struct PendingFree {
+    void* p;
+    std::vector<hipEvent_t> ev;
+  };
   hipMemPool_t pool = nullptr;
-  hipStream_t astream = nullptr, fstream = nullptr;
+  hipStream_t astream = nullptr;
   std::set<void*> pool_ptrs;
-  std::vector<hipEvent_t> fence_ev;
+  std::vector<PendingFree> pending_frees;
+  std::vector<hipEvent_t> spare_ev;
   // Device scratch (rec, prefix, ksort, okb, order_scratch) is shared by
   // calls on d.stream and on caller streams (the *_dev entry points).  The
   // mutex orders the enqueues; this event orders the execution: a call on a
@@ -562,6 +568,21 @@ hipError_t fence_reader(Device& d, hipStream_t st) {
 }
 
 void qc_keeper_loop(Device* d);
+
+// The latency stream (launched latency-path kernels, small digest calls) has
+// the highest priority: HIP keeps high-priority streams on hardware queues of
+// their own, so a certificate launched beside a batch is never queued behind
+// it in a hardware queue that the batch's stream shares (with more streams
+// than GPU_MAX_HW_QUEUES, normal-priority streams share queues), and the CP
+// dispatches it first.
+hipError_t ensure_lstream(Device& d) {
+  if (d.lstream) return hipSuccess;
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+      hipStreamCreateWithPriority(&d.lstream, hipStreamNonBlocking, hi) == hipSuccess)
+    return hipSuccess;
+  return hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking);
+}
 
 // arm the wide kernel (kQcCap waves) while calls of 9..kQcCap signatures keep
 // coming (PBFTV_QC_KEEP_MS since the last one; PBFTV_QC_WIDE=0: never).  Its
@@ -1100,17 +1121,23 @@ void pbftv_close(pbftv_ctx* ctx) {
       if (d->h2d_ev[k]) (void)hipEventDestroy(d->h2d_ev[k]);
       if (d->comp_ev[k]) (void)hipEventDestroy(d->comp_ev[k]);
     }
-    if (d->pool) {  // blocks the caller did not free go with the context
+    if (d->pool) {  // pending frees and blocks the caller did not free go with the context
       GpuQuiesce quiet(d->id);
-      for (void* p : d->pool_ptrs) (void)hipFreeAsync(p, d->fstream);
+      for (auto& pf : d->pending_frees) {
+        for (hipEvent_t e : pf.ev) {
+          (void)hipEventSynchronize(e);
+          d->spare_ev.push_back(e);
+        }
+        (void)hipFreeAsync(pf.p, d->astream);
+      }
+      d->pending_frees.clear();
+      for (void* p : d->pool_ptrs) (void)hipFreeAsync(p, d->astream);
       d->pool_ptrs.clear();
-      (void)hipStreamSynchronize(d->fstream);
       (void)hipStreamSynchronize(d->astream);
       (void)hipMemPoolDestroy(d->pool);
-      (void)hipStreamDestroy(d->fstream);
       (void)hipStreamDestroy(d->astream);
     }
-    for (hipEvent_t e : d->fence_ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : d->spare_ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
   }
   if (!ctx->host_cache.empty()) {
@@ -1151,10 +1178,10 @@ static Device* dev_of(pbftv_ctx* ctx, int dev) {
 
 // The device pool of pbftv_dev_alloc: memory is never returned to the
 // driver while the context lives (release threshold: unlimited), so a free
-// is a stream-ordered bookkeeping step, not hipFree (which waits for every
-// kernel on the GPU, the armed servers included).  Allocations are made on
-// astream and reuse only blocks whose free has completed (no reuse that would
-// make an allocation wait for a pending free); frees go on fstream.
+// is bookkeeping, not hipFree (which waits for every kernel on the GPU, the
+// armed servers included).  Allocations are made on astream and reuse only
+// blocks whose free has completed (no reuse that would make an allocation
+// wait for a pending free).
 static hipError_t dev_pool_ready(Device& d) {
   if (d.pool) return hipSuccess;
   hipMemPoolProps props{};
@@ -1169,30 +1196,60 @@ static hipError_t dev_pool_ready(Device& d) {
   HIP_TRY_E(hipMemPoolSetAttribute(d.pool, hipMemPoolReuseAllowInternalDependencies, &no));
   HIP_TRY_E(hipMemPoolSetAttribute(d.pool, hipMemPoolReuseFollowEventDependencies, &no));
   HIP_TRY_E(hipStreamCreateWithFlags(&d.astream, hipStreamNonBlocking));
-  HIP_TRY_E(hipStreamCreateWithFlags(&d.fstream, hipStreamNonBlocking));
   return hipSuccess;
 }
 
-// fstream waits, on the GPU, for everything the context may still run on a
-// buffer: its own streams, its library streams and every caller stream it
-// was given (the scratch fence and the reader fences) -- no host wait.
-static hipError_t fence_free_stream(Device& d) {
-  std::vector<hipStream_t> sts;
-  for (hipStream_t s : {d.stream, d.stream2, d.cstream, d.lstream})
-    if (s) sts.push_back(s);
-  for (auto& kv : d.stream_scratch) sts.push_back(kv.first);
-  while (d.fence_ev.size() < sts.size()) {
+// A free: events on the context's own streams and its library streams
+// (pbftv_stream_create) mark what may still use the block; no stream waits
+// for them (a wait packet would stall every stream sharing that stream's
+// hardware queue).  Work the context put on CALLER streams (the scratch fence
+// and the reader fences of *_dev calls on streams it did not create) is waited
+// for on the host here, as hipFree's implicit synchronisation would -- only
+// that work, not the whole GPU.
+static hipError_t defer_free(Device& d, void* p) {
+  if (d.scratch_st && d.scratch_st != d.stream && !d.stream_scratch.count(d.scratch_st) && d.scratch_ev)
+    HIP_TRY_E(hipEventSynchronize(d.scratch_ev));
+  for (auto& kv : d.reader_ev) HIP_TRY_E(hipEventSynchronize(kv.second));
+  Device::PendingFree pf{p, {}};
+  auto mark = [&](hipStream_t st) -> hipError_t {
     hipEvent_t e;
-    HIP_TRY_E(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    d.fence_ev.push_back(e);
+    if (!d.spare_ev.empty()) {
+      e = d.spare_ev.back();
+      d.spare_ev.pop_back();
+    } else {
+      HIP_TRY_E(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    pf.ev.push_back(e);
+    return hipEventRecord(e, st);
+  };
+  for (hipStream_t st : {d.stream, d.stream2, d.cstream, d.lstream})
+    if (st) HIP_TRY_E(mark(st));
+  for (auto& kv : d.stream_scratch) HIP_TRY_E(mark(kv.first));
+  d.pending_frees.push_back(std::move(pf));
+  return hipSuccess;
+}
+
+// return the blocks whose marks have all passed to the pool (host polls)
+static hipError_t reap_frees(Device& d) {
+  size_t k = 0;
+  for (auto& pf : d.pending_frees) {
+    bool done = true;
+    for (hipEvent_t e : pf.ev) {
+      const hipError_t q = hipEventQuery(e);
+      if (q == hipErrorNotReady) {
+        done = false;
+        break;
+      }
+      if (q != hipSuccess) return q;
+    }
+    if (!done) {
+      d.pending_frees[k++] = std::move(pf);
+      continue;
+    }
+    for (hipEvent_t e : pf.ev) d.spare_ev.push_back(e);
+    HIP_TRY_E(hipFreeAsync(pf.p, d.astream));
   }
-  for (size_t i = 0; i < sts.size(); ++i) {
-    HIP_TRY_E(hipEventRecord(d.fence_ev[i], sts[i]));
-    HIP_TRY_E(hipStreamWaitEvent(d.fstream, d.fence_ev[i], 0));
-  }
-  if (d.scratch_st && d.scratch_st != d.stream && d.scratch_ev)
-    HIP_TRY_E(hipStreamWaitEvent(d.fstream, d.scratch_ev, 0));
-  for (auto& kv : d.reader_ev) HIP_TRY_E(hipStreamWaitEvent(d.fstream, kv.second, 0));
+  d.pending_frees.resize(k);
   return hipSuccess;
 }
 
@@ -1202,6 +1259,7 @@ int pbftv_dev_alloc(pbftv_ctx* ctx, int dev, uint64_t bytes, void** out_ptr) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
   HIP_TRY(dev_pool_ready(*d));
+  HIP_TRY(reap_frees(*d));
   HIP_TRY(hipMallocFromPoolAsync(out_ptr, bytes ? bytes : 1, d->pool, d->astream));
   HIP_TRY(hipStreamSynchronize(d->astream));  // (usable on any stream once this returns)
   d->pool_ptrs.insert(*out_ptr);
@@ -1268,11 +1326,11 @@ int pbftv_dev_free(pbftv_ctx* ctx, int dev, void* ptr) {
   HIP_TRY(hipSetDevice(d->id));
   auto it = d->pool_ptrs.find(ptr);
   if (it != d->pool_ptrs.end()) {
-    // stream-ordered: the block returns to the pool once the context's work
-    // queued so far has passed (fstream waits for it on the GPU)
+    // the block returns to the pool once the context's work queued so far
+    // has passed (defer_free / reap_frees)
     d->pool_ptrs.erase(it);
-    HIP_TRY(fence_free_stream(*d));
-    HIP_TRY(hipFreeAsync(ptr, d->fstream));
+    HIP_TRY(defer_free(*d, ptr));
+    HIP_TRY(reap_frees(*d));
     return PBFTV_OK;
   }
   GpuQuiesce quiet(d->id);  // (not from the pool) hipFree waits for every kernel on the GPU: armed ones leave first
@@ -2030,7 +2088,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       std::memcpy(sp, sig_rs, 64 * n);
       std::memcpy(kp, key_idx, 4 * n);
       HIP_TRY(set_dev());
-      if (!d.lstream) HIP_TRY(hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking));
+      HIP_TRY(ensure_lstream(d));
       HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.lstream, [&] {
         return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n, d.key_valid.as<uint32_t>(), d.nkeys,
                                         d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,
@@ -2342,7 +2400,7 @@ static int sha_host_small(Device& d, const uint8_t* data, const uint64_t* offset
   for (uint64_t i = 0; i < n; ++i) off[i] = offsets[i] - lo_b;
   std::memcpy(b + o_len, lengths, 4 * n);
   if (span) std::memcpy(b + o_data, data + lo_b, span);
-  if (!d.lstream) HIP_TRY(hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking));
+  HIP_TRY(ensure_lstream(d));
   HIP_TRY(timed(d, PBFTV_K_SHA256, d.lstream, [&] {
     return pbftv::launch_sha256(b + o_data, off, reinterpret_cast<const uint32_t*>(b + o_len), nullptr, n, b + o_dig,
                                 nullptr, nullptr, d.lstream);

@@ -20,25 +20,6 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
 
 
-@pytest.fixture(autouse=True)
-def _frees_between_gpu_tests(request):
-    """A GPU test's frees happen in the test: earlier tests' cyclic garbage
-    (device / pinned buffers) is collected before it and none during it --
-    every library free quiesces the GPU (halts the armed servers, DESIGN.md
-    3.8.1), so a collection in the middle of a test that checks which path
-    served a certificate would make it depend on the collector's timing."""
-    if request.node.get_closest_marker("gpu") is None:
-        yield
-        return
-    import gc
-    gc.collect()
-    gc.disable()
-    try:
-        yield
-    finally:
-        gc.enable()
-
-
 def _load_json(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)
