@@ -247,6 +247,7 @@ struct Device {
   std::shared_ptr<DevBuf> gtab;  // shared by every context on this GPU at this width (g_tables)
   DevBuf key_valid, qptrs;
   DevBuf tab_scratch[6];  // table build: bases, L, H, phase-2 / phase-3 scratch, table addresses
+  DevBuf tab_keys;        // table build: the keys' coordinates
   std::vector<std::unique_ptr<DevBuf>> qblocks;
   std::vector<void*> qtab;  // table of key j (registered keys first, then spare slots)
   int gbits = 0, qbits = 0;
@@ -569,19 +570,45 @@ hipError_t fence_reader(Device& d, hipStream_t st) {
 
 void qc_keeper_loop(Device* d);
 
-// The latency stream (launched latency-path kernels, small digest calls) has
-// the highest priority: HIP keeps high-priority streams on hardware queues of
-// their own, so a certificate launched beside a batch is never queued behind
-// it in a hardware queue that the batch's stream shares (with more streams
-// than GPU_MAX_HW_QUEUES, normal-priority streams share queues), and the CP
-// dispatches it first.
-hipError_t ensure_lstream(Device& d) {
-  if (d.lstream) return hipSuccess;
-  int lo = 0, hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-      hipStreamCreateWithPriority(&d.lstream, hipStreamNonBlocking, hi) == hipSuccess)
-    return hipSuccess;
-  return hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking);
+// The armed kernels' two streams, at the HIGHEST priority: HIP keeps
+// high-priority streams on hardware queues of their own (the normal ones are
+// shared once a process has more streams than GPU_MAX_HW_QUEUES), and a
+// kernel that stays resident on a normal-priority queue makes every
+// synchronous null-stream operation on the GPU (hipMemcpy, a caller's or this
+// library's) wait until it ends -- a full budget (tools/queue_share.hip,
+// profiles/r05_queue_share.txt).  The CP also dispatches them first.
+hipError_t qc_streams_ready(Device& d) {
+  for (hipStream_t& q : d.qstream) {
+    if (q) continue;
+    int lo = 0, hi = 0;
+    const char* pe = getenv("PBFTV_QC_PRIO");  // (experiments) "0": normal-priority armed streams
+    if ((pe && pe[0] == '0') || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi) != hipSuccess)
+      HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+  }
+  return hipSuccess;
+}
+
+// Where a latency-path kernel is LAUNCHED (a certificate the armed server
+// cannot take, its exact rerun, a small digest call): the armed stream that
+// holds no resident kernel -- a hardware queue of its own, never behind a
+// batch (a normal stream may share its hardware queue with the stream the
+// batches are queued on), dispatched first; the next arming queues behind the
+// short launched kernel.  While a rotation keeps both armed streams resident,
+// the normal-priority latency stream (lstream).  No extra high-priority
+// stream: their hardware queues are few too, and a stream sharing one with a
+// resident armed kernel would wait for that kernel's budget.
+hipError_t latency_stream(Device& d, hipStream_t* out) {
+  HIP_TRY_E(qc_streams_ready(d));
+  if (!d.arm_seq) {
+    *out = d.qstream[0];
+  } else if (!d.retiring) {
+    *out = d.qstream[d.arm_stream ^ 1];
+  } else {
+    if (!d.lstream) HIP_TRY_E(hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking));
+    *out = d.lstream;
+  }
+  return hipSuccess;
 }
 
 // arm the wide kernel (kQcCap waves) while calls of 9..kQcCap signatures keep
@@ -601,20 +628,7 @@ hipError_t qc_arm(Device& d) {
   if (d.arm_seq || !qc_arm_enabled() || !d.have_keys) return hipSuccess;
   if (qc_yield() && lane_busy(d)) return hipSuccess;  // the keeper arms once the batches are done
   HIP_TRY_E(qc_mail_ready(d));
-  // The armed kernels' streams have the HIGHEST priority: HIP keeps
-  // high-priority streams on hardware queues of their own, and a kernel that
-  // stays resident on a normal-priority queue makes every synchronous
-  // null-stream operation on the GPU (hipMemcpy, a caller's or this
-  // library's) wait until it ends -- a full budget (tools/queue_share.hip,
-  // profiles/r05_queue_share.txt).  The CP also dispatches them first.
-  for (hipStream_t& q : d.qstream) {
-    if (q) continue;
-    int lo = 0, hi = 0;
-    const char* pe = getenv("PBFTV_QC_PRIO");  // (experiments) "0": normal-priority armed streams
-    if ((pe && pe[0] == '0') || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi) != hipSuccess)
-      HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-  }
+  HIP_TRY_E(qc_streams_ready(d));
   uint32_t halt;
   {
     // the check and the halt snapshot in one critical section: a quiesce that
@@ -1086,6 +1100,7 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)collect_times(*d);
     for (auto& b : d->qblocks) b->release();
     for (auto& b : d->tab_scratch) b.release();
+    d->tab_keys.release();
     d->gtab.reset();
     d->vs.release();
     for (DevBuf* b : {&d->qptrs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx,
@@ -1600,11 +1615,13 @@ static int build_key_tables(Device& d, const std::vector<uint32_t>& le, uint32_t
   }
   std::vector<void*> tabs(k);
   for (uint32_t j = 0; j < k; ++j) tabs[j] = d.qtab[key0 + j];
-  DevBuf keys;
-  HIP_TRY(keys.ensure((size_t)k * 64 + 64));
-  HIP_TRY(hipMemcpyAsync(keys.p, le.data(), (size_t)k * 64, hipMemcpyHostToDevice, d.stream));
+  // the keys' coordinates: a grow-only buffer of the device (a temporary's
+  // free would quiesce the GPU -- halt every armed server on it -- at every
+  // pbftv_set_key / pbftv_add_keys)
+  HIP_TRY(d.tab_keys.ensure((size_t)k * 64 + 64));
+  HIP_TRY(hipMemcpyAsync(d.tab_keys.p, le.data(), (size_t)k * 64, hipMemcpyHostToDevice, d.stream));
   if (k) {
-    int rc = build_tables(d, d.qbits, keys.as<uint32_t>(), key0, k, 0, d.key_valid.as<uint32_t>(), tabs);
+    int rc = build_tables(d, d.qbits, d.tab_keys.as<uint32_t>(), key0, k, 0, d.key_valid.as<uint32_t>(), tabs);
     if (rc != PBFTV_OK) return rc;
   }
   trace("key table build", d.id, t0);
@@ -2079,6 +2096,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     m->cap = cap;
     m->n = (uint32_t)n;
     ++d.qc_calls;
+    hipStream_t lst = nullptr;  // where this call's launched kernel went (latency_stream)
     auto launch_plain = [&]() -> int {
       ++d.qc_launches;
       uint8_t* const hp = st8 + QcMail::hashes_off(cap);
@@ -2088,11 +2106,11 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       std::memcpy(sp, sig_rs, 64 * n);
       std::memcpy(kp, key_idx, 4 * n);
       HIP_TRY(set_dev());
-      HIP_TRY(ensure_lstream(d));
-      HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, d.lstream, [&] {
+      HIP_TRY(latency_stream(d, &lst));
+      HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, lst, [&] {
         return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n, d.key_valid.as<uint32_t>(), d.nkeys,
                                         d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,
-                                        const_cast<uint8_t*>(res), d.lstream);
+                                        const_cast<uint8_t*>(res), lst);
       }));
       return PBFTV_OK;
     };
@@ -2207,7 +2225,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         // no stale verdict can land in the next call's result bytes
         HIP_TRY(set_dev());
         HIP_TRY(qc_disarm(d));
-        if (d.lstream) HIP_TRY(hipStreamSynchronize(d.lstream));
+        if (lst) HIP_TRY(hipStreamSynchronize(lst));
         bool missing = false;
         for (uint64_t i = next; i < n; ++i) missing |= res[i] == 0xFF;
         if (!missing) break;
@@ -2239,7 +2257,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         std::memset(const_cast<uint8_t*>(res), 0xFF, n);
         int rc = launch_plain();
         if (rc != PBFTV_OK) return rc;
-        HIP_TRY(hipStreamSynchronize(d.lstream));
+        HIP_TRY(hipStreamSynchronize(lst));
         for (uint64_t i = 0; i < n; ++i)
           if (res[i] == 0xFF) return fail(PBFTV_EDEVICE, "wave verify kernel did not report every signature");
       }
@@ -2400,12 +2418,13 @@ static int sha_host_small(Device& d, const uint8_t* data, const uint64_t* offset
   for (uint64_t i = 0; i < n; ++i) off[i] = offsets[i] - lo_b;
   std::memcpy(b + o_len, lengths, 4 * n);
   if (span) std::memcpy(b + o_data, data + lo_b, span);
-  HIP_TRY(ensure_lstream(d));
-  HIP_TRY(timed(d, PBFTV_K_SHA256, d.lstream, [&] {
+  hipStream_t lst = nullptr;
+  HIP_TRY(latency_stream(d, &lst));
+  HIP_TRY(timed(d, PBFTV_K_SHA256, lst, [&] {
     return pbftv::launch_sha256(b + o_data, off, reinterpret_cast<const uint32_t*>(b + o_len), nullptr, n, b + o_dig,
-                                nullptr, nullptr, d.lstream);
+                                nullptr, nullptr, lst);
   }));
-  HIP_TRY(hipStreamSynchronize(d.lstream));
+  HIP_TRY(hipStreamSynchronize(lst));
   std::memcpy(out_digests, b + o_dig, 32 * n);
   return PBFTV_OK;
 }

@@ -734,7 +734,7 @@ def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypa
                 assert call(v, 12)
         for v in (a, b):
             c1 = v.qc_counters(0)
-            assert c1["armings"] == c0[id(v)]["armings"] and c1["armed"] - c0[id(v)]["armed"] == 20, (c0[id(v)], c1)
+            assert c1["armed"] - c0[id(v)]["armed"] == 20 and c1["launches"] == c0[id(v)]["launches"], (c0[id(v)], c1)
         t0 = time.perf_counter()
         assert b.set_key(1, keys[1])  # b's key change with a's kernel armed (b waits for b's work only)
         assert time.perf_counter() - t0 < 2.0

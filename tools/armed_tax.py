@@ -32,9 +32,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=0.4)
     ap.add_argument("--sizes", default="1048576,1032192,983040")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="2: four batches alternating over two library streams per sync (bench.py's step); "
+                         "1: two batches on one stream per sync (bench.py qc_under_load's stream)")
+    ap.add_argument("--arm-ms", default="200", help="PBFTV_QC_ARM_MS (the keeper rotates every half of it)")
+    ap.add_argument("--configs", default="none,rows_narrow_4,rows_narrow_1,rows_wide,quad_narrow")
     a = ap.parse_args()
-    os.environ["PBFTV_QC_KEEP_MS"] = "1200"  # the keeper drops the server 1.2 s after the last call
-    os.environ["PBFTV_QC_ARM_MS"] = "200"
+    os.environ["PBFTV_QC_KEEP_MS"] = str(max(1200, 3 * int(a.arm_ms)))  # the keeper drops the server after this
+    os.environ["PBFTV_QC_ARM_MS"] = a.arm_ms
     import synth  # noqa: E402
     from simple_pbft_amd import Verifier  # noqa: E402
     n = 1 << 20
@@ -67,13 +72,15 @@ def main():
 
         def run():
             j = 0
+            per = 4 if a.streams == 2 else 2
             while not stop.is_set():
-                for _ in range(4):
-                    ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, m, dbs[j & 1].ptr, stream=sts[j & 1])
+                for _ in range(per):
+                    k = j & 1 if a.streams == 2 else 0
+                    ver.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, m, dbs[k].ptr, stream=sts[k])
                     j += 1
                 for st in sts:
                     ver.stream_wait(0, st)
-                done[0] += 4
+                done[0] += per
         th = threading.Thread(target=run)
         th.start()
         time.sleep(0.08)
@@ -92,7 +99,7 @@ def main():
     def arm(cfg):
         """make the keeper hold the kernel of this configuration, then no call"""
         set_env(cfg["env"])
-        time.sleep(1.6)  # whatever was armed has been dropped (keep 1.2 s + budget)
+        time.sleep(int(os.environ["PBFTV_QC_KEEP_MS"]) * 1e-3 + 2 * int(a.arm_ms) * 1e-3 + 0.2)  # the last arming ran out
         if cfg["cert"] == 0:
             return {}
         for _ in range(3):
@@ -107,6 +114,8 @@ def main():
         {"name": "rows_wide", "env": {}, "cert": 67},
         {"name": "quad_narrow", "env": {"PBFTV_QC_ROWS": "0", "PBFTV_QC_WIDE": "0"}, "cert": 3},
     ]
+    want = a.configs.split(",")
+    configs = [c for c in configs if c["name"] in want]
     res = {c["name"]: {str(m): [] for m in sizes} for c in configs}
     shape = {}
     rate(n, 0.3)  # warm
@@ -118,11 +127,12 @@ def main():
             print(json.dumps({"round": rnd, "cfg": cfg["name"], "rates": {m: res[cfg["name"]][str(m)][-1]
                                                                            for m in map(str, sizes)}}),
                   file=sys.stderr, flush=True)
-    out = {"rates": {k: {m: float(np.mean(v)) for m, v in d.items()} for k, d in res.items()}, "shape": shape}
+    out = {"rates": {k: {m: float(np.mean(v)) for m, v in d.items()} for k, d in res.items()}, "shape": shape,
+           "streams": a.streams, "arm_ms": a.arm_ms}
     base = out["rates"]["none"]
     out["ratio_to_none"] = {k: {m: out["rates"][k][m] / base[m] for m in base} for k in out["rates"]}
     out["check"] = all(bool((np.unpackbits(db.to_host(), bitorder="little")[:sizes[-1]].astype(bool) ==
-                             ok[:sizes[-1]]).all()) for db in dbs)
+                             ok[:sizes[-1]]).all()) for db in dbs[:a.streams])
     print(json.dumps(out), flush=True)
     ver.close()
 
