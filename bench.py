@@ -552,7 +552,7 @@ def qc_under_load(ver: Verifier, dh, ds, dk, n: int, ok, seed: int, calls3: int 
     128-wave kernel.  The stream's rate alone (no certificate, nothing armed
     yet) is measured first, for the ratio."""
     import threading
-    _, H3, S3, K3 = synth.certs(100, 3, 2 * calls3 + 40, seed)
+    _, H3, S3, K3 = synth.certs(100, 3, 2 * calls3 + 80, seed)
     _, H67, S67, K67 = synth.certs(100, 67, 2 * calls67 + 20, seed)
 
     def part(H, S, K, sigs, lo, cnt):
@@ -584,19 +584,49 @@ def qc_under_load(ver: Verifier, dh, ds, dk, n: int, ok, seed: int, calls3: int 
             stop.set()
             th.join()
         return r, rate
-    out = {}
+    def forced(fn):
+        """fn() with PBFTV_QC_YIELD=0: a server stays resident beside the batches"""
+        saved = os.environ.get("PBFTV_QC_YIELD")
+        os.environ["PBFTV_QC_YIELD"] = "0"
+        try:
+            return fn()
+        finally:
+            if saved is None:
+                os.environ.pop("PBFTV_QC_YIELD", None)
+            else:
+                os.environ["PBFTV_QC_YIELD"] = saved
+
+    out = {"yield_policy": os.environ.get("PBFTV_QC_YIELD", "adaptive (PBFTV_QC_YIELD unset: a batch halts the "
+                                          "server when no certificate came for PBFTV_QC_YIELD_IDLE_MS = 50 ms)")}
     _, out["stream_verifies_per_s_alone"] = loaded(lambda: time.sleep(0.6))
     out["idle_3sigs"] = part(H3, S3, K3, 3, 0, calls3)
     out["loaded_3sigs"], r3 = loaded(lambda: part(H3, S3, K3, 3, calls3 + 20, calls3))
-    # the stream again with the 8-wave kernel armed (the keeper holds it) and no certificate
-    _, out["stream_verifies_per_s_armed_narrow"] = loaded(lambda: time.sleep(0.6))
+    # the stream right after those certificates, no call meanwhile: the default
+    # policy (the first batch after 50 ms without a certificate halts the server) ...
+    _, out["stream_verifies_per_s_after_3sigs_no_calls"] = loaded(lambda: time.sleep(0.6))
+    # ... and with the narrow server held resident beside it (PBFTV_QC_YIELD=0)
+    def narrow_resident():
+        part(H3, S3, K3, 3, 2 * calls3 + 30, 2)
+        return loaded(lambda: time.sleep(0.6))[1]
+    out["stream_verifies_per_s_armed_narrow"] = forced(narrow_resident)
+    # sparse certificates (one per 100 ms) while the stream runs: the default
+    # policy serves each with a launch beside the batches (the server was halted)
+    out["loaded_3sigs_every_100ms"], _ = loaded(lambda: qc_latency(
+        ver, 100, 3, 20, 0, gap_s=0.1, warm=2,
+        certs=(H3[3 * (calls3 + 2):], S3[3 * (calls3 + 2):], K3[3 * (calls3 + 2):])))
     out["idle_67sigs"] = part(H67, S67, K67, 67, 0, calls67)
     out["loaded_67sigs"], r67 = loaded(lambda: part(H67, S67, K67, 67, calls67 + 10, calls67))
+
+    def wide_resident():
+        part(H67, S67, K67, 67, 0, 2)
+        return loaded(lambda: time.sleep(0.6))[1]
+    out["stream_verifies_per_s_armed_wide"] = forced(wide_resident)
     out["stream_verifies_per_s_during"] = {"3sigs": r3, "67sigs": r67}
-    out["stream_rate_ratio"] = {"3sigs": r3 / out["stream_verifies_per_s_alone"],
-                                "67sigs": r67 / out["stream_verifies_per_s_alone"],
-                                "armed_narrow_no_calls": out["stream_verifies_per_s_armed_narrow"] /
-                                out["stream_verifies_per_s_alone"]}
+    alone = out["stream_verifies_per_s_alone"]
+    out["stream_rate_ratio"] = {"3sigs": r3 / alone, "67sigs": r67 / alone,
+                                "after_3sigs_no_calls": out["stream_verifies_per_s_after_3sigs_no_calls"] / alone,
+                                "armed_narrow_no_calls": out["stream_verifies_per_s_armed_narrow"] / alone,
+                                "armed_wide_no_calls": out["stream_verifies_per_s_armed_wide"] / alone}
     out["stream_check"] = bool((np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool) == ok).all())
     db.free()
     ver.stream_destroy(0, st)

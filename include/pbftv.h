@@ -68,13 +68,20 @@ int pbftv_reserve(pbftv_ctx* ctx, uint64_t n);
 
 /* ---- device memory / stream plumbing ---------------------------------- */
 /* For callers that keep pool snapshots resident in HBM (and for bench.py):
- * plain allocations on the context's device index dev, copies on that
- * device's stream (synchronous), and a stream synchronise. */
+ * allocations on the context's device index dev, copies on that device's
+ * stream (synchronous), and a stream synchronise.  pbftv_dev_alloc memory
+ * comes from a stream-ordered pool of the context; pbftv_dev_free returns it
+ * once the work queued so far on the context's streams (its own and those
+ * from pbftv_stream_create) has passed, without a device-wide
+ * synchronisation, and waits on the host for the context's work on other
+ * caller streams -- so a free does not stop the armed latency kernels. */
 int pbftv_dev_alloc(pbftv_ctx* ctx, int dev, uint64_t bytes, void** out_ptr);
 int pbftv_dev_free(pbftv_ctx* ctx, int dev, void* ptr);
 /* Pinned host memory (hipHostMalloc, portable): batches placed in it skip the
  * staging copy of the host-buffer verify path (e.g. a cgo shim's pool-flush
- * buffers). */
+ * buffers).  A freed block is kept for the next pbftv_host_alloc of a similar
+ * size (up to 1 GiB per context; released at pbftv_close), so a free does
+ * not synchronise the GPU either. */
 int pbftv_host_alloc(pbftv_ctx* ctx, uint64_t bytes, void** out_ptr);
 int pbftv_host_free(pbftv_ctx* ctx, void* ptr);
 int pbftv_memcpy_h2d(pbftv_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes);
@@ -102,9 +109,10 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
  * path.
  *
  * Up to 128 signatures of a latency-path call are served by a resident
- * "armed" kernel polling a doorbell in pinned host memory (8 slot waves; 120
- * helper waves more once calls of 9..128 signatures have been seen), so no
- * launch is on the call's path.  A keeper thread per device replaces it
+ * "armed" kernel polling a doorbell in pinned host memory (a workgroup per
+ * signature slot: as many as the largest recent certificate, at least 4;
+ * up to 128 once calls of 9..128 signatures have been seen), so no launch is
+ * on the call's path.  A keeper thread per device replaces it
  * before its budget runs out for as long as calls keep coming.  Environment,
  * read at every arming:
  *   PBFTV_QC_ARM=0            never arm (every call launches);
@@ -112,12 +120,14 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
  *   PBFTV_QC_KEEP_MS=10000    keep one armed this long after the last call
  *                             (0: no keeper; the kernel runs out);
  *   PBFTV_QC_WIDE=0           never arm the 128-wave form;
- *   PBFTV_QC_YIELD=1          no armed kernel while lane-path batches
- *                             run: a batch enqueue halts it, certificates
- *                             meanwhile are launched (slower beside the
- *                             batch), the keeper re-arms after it.  Any
- *                             resident kernel slows a busy stream by 3-7 %
- *                             on this hardware; off by default;
+ *   PBFTV_QC_YIELD            whether a lane-path batch halts the armed
+ *                             kernel (certificates meanwhile are launched,
+ *                             ~0.3 ms beside the batch instead of ~0.05 ms;
+ *                             the keeper re-arms after it): "1" always, "0"
+ *                             never; unset (default) when no certificate
+ *                             came for PBFTV_QC_YIELD_IDLE_MS (50 ms).  A
+ *                             resident server costs a busy stream ~3 %
+ *                             (narrow) to 6-9 % (wide, 67 votes);
  *   PBFTV_QC_EXCLUSIVE_CU     armed workgroups take whole CUs, so a
  *                             concurrent batch does not share their SIMDs
  *                             (with PBFTV_QC_YIELD=0): "narrow" the narrow
@@ -131,9 +141,11 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
  *   PBFTV_QC_SLOTS=k          arm k narrow slots (1..8) instead of the
  *                             largest recent certificate (at least 4);
  *   PBFTV_QC_STAMPS=1         the kernel records GPU timestamps
- *                             (pbftv_qc_stamps*).
- * pbftv_dev_free / pbftv_host_free and the library's own frees stop every
- * armed kernel on the GPU first (hipFree waits for every kernel). */
+ *                             (pbftv_qc_stamps*);
+ *   PBFTV_TRACE_QC=1          why a call was launched, on stderr.
+ * The library's own device frees (scratch growth, re-registration) stop every
+ * armed kernel on the GPU first (hipFree waits for every kernel); the
+ * caller's pbftv_dev_free / pbftv_host_free do not. */
 int pbftv_set_latency_path_max(pbftv_ctx* ctx, uint64_t n);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every

@@ -435,19 +435,31 @@ uint32_t qc_spin() {
   return e ? (uint32_t)atoi(e) : 0u;
 }
 
-// PBFTV_QC_YIELD=1 (opt-in): no armed kernel stays resident while lane-path
-// batches are queued on its device.  Any kernel resident on another queue
-// slows a busy stream's kernels by 3-7 % on this hardware, even one that only
-// sleeps (tools/persist_cost.hip, profiles/r05_persist_cost.txt), so a
-// certificate server armed beside a large flush costs the flush that much.
-// With yield, a batch enqueue halts the armed kernel, a certificate in the
-// meantime is served by a launch on the latency stream, and the keeper arms
-// again once the queued batches are expected to be done.  Off by default: a
-// certificate launched beside a batch waits for free wave slots (~0.28 ms
-// instead of ~0.055 ms armed, profiles/r05_qc_yield_ab.txt).
-bool qc_yield() {
+// Whether an armed kernel yields to lane-path batches (PBFTV_QC_YIELD).  A
+// kernel resident beside a busy stream costs it its wave slots: the narrow
+// row server (4 workgroups) ~3 %, the wide one (a workgroup per signature of
+// the largest recent wide certificate, 72 for 67 votes) 6-9 %
+// (tools/armed_tax.py, profiles/r06_armed_tax_*.json).  A yielding server is
+// halted by the batch enqueue (note_busy); a certificate in the meantime is
+// launched on the free armed stream (it waits for free wave slots beside the
+// batch, ~0.3 ms instead of ~0.05 ms), and the keeper arms again once the
+// queued batches are expected to be done.
+//   "1": always yield;  "0": never (a server stays resident beside batches);
+//   unset (the default): yield while certificates are sparse -- when none has
+//   come for PBFTV_QC_YIELD_IDLE_MS (default 50 ms).  A node whose
+//   certificates keep coming (every few ms) keeps its server resident beside
+//   its flushes; one that checks a certificate now and then does not pay for
+//   a resident server during every flush in between.
+int qc_yield_mode() {
   const char* e = getenv("PBFTV_QC_YIELD");
-  return e && e[0] == '1';
+  return e ? (e[0] == '1' ? 1 : 0) : 2;
+}
+
+bool qc_yield_now(const Device& d) {
+  const int m = qc_yield_mode();
+  if (m != 2) return m == 1;
+  const auto idle = std::chrono::microseconds((int64_t)(env_ms("PBFTV_QC_YIELD_IDLE_MS", 50.0) * 1000.0));
+  return std::chrono::steady_clock::now() - d.last_qc > idle;
 }
 
 // PBFTV_QC_SLOTS=k (1..kQcSlots): every narrow arming takes k slots; 0: unset
@@ -626,7 +638,7 @@ bool qc_wide_wanted(const Device& d) {
 // a quiesce of this GPU is in progress: the request then takes a launch).
 hipError_t qc_arm(Device& d) {
   if (d.arm_seq || !qc_arm_enabled() || !d.have_keys) return hipSuccess;
-  if (qc_yield() && lane_busy(d)) return hipSuccess;  // the keeper arms once the batches are done
+  if (qc_yield_now(d) && lane_busy(d)) return hipSuccess;  // the keeper arms once the batches are done
   HIP_TRY_E(qc_mail_ready(d));
   HIP_TRY_E(qc_streams_ready(d));
   uint32_t halt;
@@ -771,7 +783,7 @@ void qc_keeper_loop(Device* d) {
     auto wake = now + far;
     qc_retire(*d);
     const int64_t busy_ns = d->busy_until_ns.load(std::memory_order_relaxed) - steady_ns();
-    if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep && qc_yield() && busy_ns > 0) {
+    if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep && qc_yield_now(*d) && busy_ns > 0) {
       // lane-path batches are queued: nothing armed until they are expected done
       wake = now + std::chrono::nanoseconds(busy_ns + 50000);
     } else if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
@@ -1841,7 +1853,7 @@ static void note_busy(Device& d, uint64_t n, double ns_per_sig = 1.1) {
   int64_t cur = d.busy_until_ns.load(std::memory_order_relaxed);
   while (!d.busy_until_ns.compare_exchange_weak(cur, std::max(cur, now) + add, std::memory_order_relaxed)) {
   }
-  if (qc_yield() && d.arm_seq && d.stage.p && d.mail_registered) {
+  if (d.arm_seq && qc_yield_now(d) && d.stage.p && d.mail_registered) {
     __atomic_add_fetch(&qc_mail(d)->halt, 1u, __ATOMIC_RELEASE);
     d.arm_seq = 0;
     d.retiring = 0;
