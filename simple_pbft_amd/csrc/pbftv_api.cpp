@@ -627,9 +627,17 @@ hipError_t latency_stream(Device& d, hipStream_t* out) {
 // coming (PBFTV_QC_KEEP_MS since the last one; PBFTV_QC_WIDE=0: never).  Its
 // 120 helper waves hold ~half a SIMD of registers each while armed, so a
 // context that only sees small certificates keeps the narrow kernel.
-bool qc_wide_wanted(const Device& d) {
+// PBFTV_QC_WIDE: "0" never arm the wide kernel (wide certificates are
+// launched), "split" never either, but split a wide certificate between the
+// armed narrow slots and one launch; unset or "1": arm the wide kernel
+int qc_wide_mode() {
   const char* e = getenv("PBFTV_QC_WIDE");
-  if (e && e[0] == '0') return false;
+  if (!e) return 1;
+  return e[0] == '0' ? 0 : e[0] == 's' ? 2 : 1;
+}
+
+bool qc_wide_wanted(const Device& d) {
+  if (qc_wide_mode() != 1) return false;
   if (d.last_wide.time_since_epoch().count() == 0) return false;
   return std::chrono::steady_clock::now() - d.last_wide < std::chrono::microseconds((int64_t)(qc_keep_ms() * 1000.0));
 }
@@ -2109,23 +2117,26 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     m->n = (uint32_t)n;
     ++d.qc_calls;
     hipStream_t lst = nullptr;  // where this call's launched kernel went (latency_stream)
-    auto launch_plain = [&]() -> int {
+    // one launch of the latency kernel for signatures [lo, n), inputs from
+    // the mailbox arrays, result bytes in place
+    auto launch_range = [&](uint64_t lo) -> int {
       ++d.qc_launches;
-      uint8_t* const hp = st8 + QcMail::hashes_off(cap);
-      uint8_t* const sp = st8 + QcMail::sigs_off(cap);
-      uint32_t* const kp = reinterpret_cast<uint32_t*>(st8 + QcMail::keys_off(cap));
-      std::memcpy(hp, hashes, 32 * n);
-      std::memcpy(sp, sig_rs, 64 * n);
-      std::memcpy(kp, key_idx, 4 * n);
+      uint8_t* const hp = st8 + QcMail::hashes_off(cap) + 32 * lo;
+      uint8_t* const sp = st8 + QcMail::sigs_off(cap) + 64 * lo;
+      uint32_t* const kp = reinterpret_cast<uint32_t*>(st8 + QcMail::keys_off(cap)) + lo;
+      std::memcpy(hp, hashes + 32 * lo, 32 * (n - lo));
+      std::memcpy(sp, sig_rs + 64 * lo, 64 * (n - lo));
+      std::memcpy(kp, key_idx + lo, 4 * (n - lo));
       HIP_TRY(set_dev());
       HIP_TRY(latency_stream(d, &lst));
       HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, lst, [&] {
-        return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n, d.key_valid.as<uint32_t>(), d.nkeys,
+        return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n - lo, d.key_valid.as<uint32_t>(), d.nkeys,
                                         d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,
-                                        const_cast<uint8_t*>(res), lst);
+                                        const_cast<uint8_t*>(res) + lo, lst);
       }));
       return PBFTV_OK;
     };
+    auto launch_plain = [&]() -> int { return launch_range(0); };
     // an armed kernel that has left (budget, cancel, halt) is collected first
     bool collected = false;
     if (d.arm_seq && __atomic_load_n(m->expired(d.arm_stream), __ATOMIC_ACQUIRE) == d.arm_seq) {
@@ -2152,9 +2163,14 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
     // a wide certificate needs every helper workgroup resident: one that is
     // still waiting for room on the GPU (beside other resident kernels) would
     // start only after the armed kernel's budget, too late to serve
-    if (d.arm_seq && n <= d.arm_waves && (n <= QcMail::kQcSlots || qc_all_live(d))) {
+    // PBFTV_QC_WIDE=split: a certificate wider than the narrow server is split
+    // -- its first signatures go to the armed slots, the rest to one launch
+    // beside them (no wide server resident between certificates)
+    const bool split = small && n > QcMail::kQcSlots && d.arm_seq && !d.arm_wide && qc_wide_mode() == 2;
+    if (d.arm_seq && (split || (n <= d.arm_waves && (n <= QcMail::kQcSlots || qc_all_live(d))))) {
       cur = d.arm_seq;
-      if (n > QcMail::kQcSlots) {  // the helpers' inputs (slots kQcSlots..n-1), before any slot tag
+      const uint64_t na = split ? std::min<uint64_t>(n, d.arm_waves) : n;  // signatures the armed kernel serves
+      if (n > QcMail::kQcSlots && !split) {  // the helpers' inputs (slots kQcSlots..n-1), before any slot tag
         std::memcpy(st8 + QcMail::hashes_off(cap) + 32 * QcMail::kQcSlots, hashes + 32 * QcMail::kQcSlots,
                     32 * (n - QcMail::kQcSlots));
         std::memcpy(st8 + QcMail::sigs_off(cap) + 64 * QcMail::kQcSlots, sig_rs + 64 * QcMail::kQcSlots,
@@ -2170,7 +2186,7 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
         uint32_t* l0 = reinterpret_cast<uint32_t*>(st8 + QcMail::slot_off(i));
         uint32_t* l1 = l0 + 16;
         uint32_t* l2 = l0 + 32;
-        if (i < n) {
+        if (i < na) {
           std::memcpy(l0 + 4, hashes + 32 * i, 32);
           std::memcpy(l1 + 4, sig_rs + 64 * i, 32);
           std::memcpy(l2 + 4, sig_rs + 64 * i + 32, 32);
@@ -2180,11 +2196,15 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
             __atomic_store_n(l, cur, __ATOMIC_RELEASE);
           }
         }
-        l0[1] = (uint32_t)n;  // a slot past n: line 0 only (its wave reads n and waits for the next)
+        l0[1] = (uint32_t)na;  // a slot past na: line 0 only (its wave reads na and waits for the next)
         __atomic_store_n(l0 + 15, cur, __ATOMIC_RELEASE);
         __atomic_store_n(l0, cur, __ATOMIC_RELEASE);
       }
       __atomic_store_n(&m->bell, cur, __ATOMIC_RELEASE);  // inputs and n are in: ring
+      if (na < n) {  // (split) the rest in one launch, beside the armed slots
+        int rc = launch_range(na);
+        if (rc != PBFTV_OK) return rc;
+      }
     } else {
       // a batch the armed kernel cannot take (n > its waves) leaves it armed
       // for the next small one; a narrow one is replaced by a wide one for the

@@ -690,6 +690,37 @@ def test_wide_arming_is_kept_by_the_keeper(oracle_lib, monkeypatch):
         assert c1["armed_wide"] and c1["armed_waves"] == 72
 
 
+def test_split_wide_certificates(oracle_lib, monkeypatch):
+    """PBFTV_QC_WIDE=split: no wide server is armed; a certificate of 9..128
+    signatures puts its first signatures into the armed narrow slots and the
+    rest into one launch beside them (pbftv_qc_counters: served armed, one
+    launch, no rerun), and the narrow server stays armed.  Corrupted votes in
+    every certificate; every bit against the oracle."""
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_WIDE", "split")
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=5, per_key=60, seed=95)
+    sigs[::5, 33] ^= 0x02
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    rng = np.random.default_rng(96)
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        for n in (3, 3):
+            o = rng.choice(n_all, n, replace=False)
+            assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all()
+        for n in (9, 20, 67, 67, 128, 100):
+            o = rng.choice(n_all, n, replace=False)
+            c0 = v.qc_counters(0)
+            assert (v.verify_batch(hashes[o], sigs[o], kidx[o]) == want[o]).all(), n
+            c1 = v.qc_counters(0)
+            assert c1["armed"] - c0["armed"] == 1, (n, c0, c1)
+            assert c1["launches"] - c0["launches"] == (1 if n > c0["armed_waves"] else 0), (n, c0, c1)
+            assert c1["reruns"] == c0["reruns"] and not c1["armed_wide"], (n, c0, c1)
+
+
 def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypatch):
     """An armed kernel with a 5-s budget stays resident between calls.  A
     device free and a pinned-host free neither wait for it nor stop it

@@ -17,7 +17,8 @@ scalars, plus rare windows and r + n < p; the golden vectors (other keys) ride
 along.  Each is served through (a) the armed narrow kernel (4-signature
 certificates), (b) the armed wide kernel (67-signature certificates, the
 crafted ones both in slot workgroups and in helpers), (c) the launched
-k_ecdsa_rows, at the 100-key geometry (29, 21), the 4-key geometry (29, 24)
+k_ecdsa_rows, (d) a 67-signature certificate split between the armed narrow
+slots and one launch (PBFTV_QC_WIDE=split), at the 100-key geometry (29, 21), the 4-key geometry (29, 24)
 and a seven-wave one (29, 20).  pbftv_qc_counters says which kernel served
 each call, that an armed call with an exceptional signature was rerun, and
 how many signatures took the launched kernel's exact path -- exactly the
@@ -132,9 +133,24 @@ def test_row_tree_exceptional_paths(gq, ecdsa_fixtures, monkeypatch):
             rows = golden[a:a + 4]
             d, exc = _call(v, rows)
             assert d["armed"] == 1 and d["exact_sigs"] == exc and d["reruns"] == (1 if exc else 0), (a, d)
+        # (d) split wide certificates (PBFTV_QC_WIDE=split): the first na
+        # signatures go to the armed narrow slots, the rest to one launch; an
+        # exceptional one among the armed part reruns the whole certificate
+        filler = (plain * 4)[:67]
+        monkeypatch.setenv("PBFTV_QC_WIDE", "split")
+        na = v.qc_counters(0)["armed_waves"]
+        assert 1 <= na <= 8 and not v.qc_counters(0)["armed_wide"]
+        for a in range(0, len(crafted), 20):
+            rows = list(filler)
+            for j, x in enumerate(crafted[a:a + 20]):
+                rows[(j * 7 + a) % 67] = x
+            d, exc = _call(v, rows)
+            head = sum(x[4] for x in rows[:na])
+            want = {"calls": 1, "armed": 1, "reruns": 1 if head else 0, "exact_sigs": exc,
+                    "launches": 2 if head else 1}
+            assert d == want, (a, d, want)
         # (b) the armed wide kernel: 67-signature certificates, crafted ones
         # at slot positions (< 8) and helper positions (>= 8)
-        filler = (plain * 4)[:67]
         monkeypatch.delenv("PBFTV_QC_WIDE")
         _wait_armed(v, filler, wide=True)  # (the first wide call is launched, the next arming is wide)
         per = 20
