@@ -341,6 +341,28 @@ func (x *Ctx) QCStamps() (QCStamps, error) {
 	return QCStamps{HandoverNs: uint64(out[0]), TotalNs: uint64(out[1]), Armed: uint64(out[2])&1 == 1}, nil
 }
 
+// QCCounters are the latency path's counters on device 0 since Open
+// (pbftv_qc_counters): calls, calls an armed kernel served, armed calls rerun
+// by a launch (an exceptional signature), signatures through a launched
+// kernel's exact path, launches, armings, keeper rotations, and the armed
+// kernel now (workgroups, 0 = none; Wide).
+type QCCounters struct {
+	Calls, Armed, Reruns, ExactSigs, Launches, Armings, Rotations uint64
+	ArmedWorkgroups                                              uint32
+	Wide                                                         bool
+}
+
+func (x *Ctx) QCCounters() (QCCounters, error) {
+	var out [8]C.uint64_t
+	err := call(func() C.int { return C.pbftv_qc_counters(x.c, 0, &out[0]) })
+	if err != nil {
+		return QCCounters{}, err
+	}
+	return QCCounters{Calls: uint64(out[0]), Armed: uint64(out[1]), Reruns: uint64(out[2]), ExactSigs: uint64(out[3]),
+		Launches: uint64(out[4]), Armings: uint64(out[5]), Rotations: uint64(out[6]),
+		ArmedWorkgroups: uint32(uint64(out[7])), Wide: uint64(out[7])>>32 == 1}, nil
+}
+
 // DERToRS is the parse half of crypto/ecdsa.VerifyASN1 (go1.19 cryptobyte
 // strictness).  A rejected encoding returns ok = false and r = s = 0, which
 // VerifySigs turns into a false, so VerifyASN1(pub, h, der) ==
