@@ -100,10 +100,16 @@ struct WaveArgs {
   const uint32_t* const* qtabs;
   uint8_t* bitmap;
   uint8_t* okbytes;
+  bool one_wave;  // the quad schedule (one 64-thread workgroup per signature) even where rows would serve
 };
+// one_wave: a workgroup of one wave per signature -- beside a batch that
+// holds every wave slot, such a workgroup starts in the first slot a finished
+// batch block frees, where a row-schedule workgroup (5-8 waves) waits for
+// several on one CU (pbftv_api.cpp launch_range)
 hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
                              uint64_t n, const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
-                             const uint32_t* const* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st);
+                             const uint32_t* const* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st,
+                             bool one_wave = false);
 // batches up to this size take the latency path (env PBFTV_WAVE_MAX overrides; 0 disables)
 uint64_t wave_path_max();
 // The latency path's result bytes (okbytes): bit 0 = the verdict; the

@@ -685,10 +685,11 @@ bool launch_wave_part_small(int wg, int wq, const WaveArgs& a, hipStream_t st);
 
 hipError_t launch_ecdsa_wave(int wg, int wq, const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx,
                              uint64_t n, const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
-                             const uint32_t* const* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
+                             const uint32_t* const* qtabs, uint8_t* bitmap, uint8_t* okbytes, hipStream_t st,
+                             bool one_wave) {
   if (n == 0) return hipSuccess;
   if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const WaveArgs a{hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes};
+  const WaveArgs a{hashes, sigs, key_idx, n, key_valid, nkeys, gtab, qtabs, bitmap, okbytes, one_wave};
   if (launch_wave_part_g29(wg, wq, a, st) || launch_wave_part_g26(wg, wq, a, st) ||
       launch_wave_part_g24(wg, wq, a, st) || launch_wave_part_small(wg, wq, a, st))
     return hipGetLastError();

@@ -407,6 +407,11 @@ bool qc_arm_enabled() {
   return e ? e[0] == '1' : true;
 }
 
+bool env_flag_default(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e ? e[0] == '1' : dflt;
+}
+
 double env_ms(const char* name, double dflt) {
   const char* e = getenv(name);
   return e ? atof(e) : dflt;
@@ -2129,10 +2134,13 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       std::memcpy(kp, key_idx + lo, 4 * (n - lo));
       HIP_TRY(set_dev());
       HIP_TRY(latency_stream(d, &lst));
+      // beside this device's lane batches: one wave per signature (a row
+      // workgroup would wait for several freed wave slots on one CU)
+      const bool one_wave = lane_busy(d) && env_flag_default("PBFTV_QC_BUSY_ONE_WAVE", true);
       HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, lst, [&] {
         return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n - lo, d.key_valid.as<uint32_t>(), d.nkeys,
                                         d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,
-                                        const_cast<uint8_t*>(res) + lo, lst);
+                                        const_cast<uint8_t*>(res) + lo, lst, one_wave);
       }));
       return PBFTV_OK;
     };

@@ -1443,6 +1443,21 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
   if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
 }
 
+// The same, compiled to at most 128 VGPRs (4 waves per SIMD, the comb's
+// budget): launched beside a lane batch (launch_wave_w one_wave), one such wave
+// fits the slot ONE finished comb wave frees, where a 175-VGPR wave needs two
+// on one SIMD -- and the batch's own blocks refill freed slots first.
+template <int WG, int WQ>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
+k_ecdsa_wave_lean(const uint8_t* __restrict__ hashes, const uint8_t* __restrict__ sigs,
+                  const uint32_t* __restrict__ key_idx, uint64_t n, const uint32_t* __restrict__ key_valid,
+                  uint32_t nkeys, const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
+                  uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+  const uint64_t i = blockIdx.x;
+  const bool ok = wave_verify_sig<WG, WQ>(hashes, sigs, key_idx, i, key_valid, nkeys, gtab, qtabs);
+  if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
+}
+
 // the row schedule, launched: one 512-thread workgroup per signature
 template <int WG, int WQ>
 __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows(const uint8_t* __restrict__ hashes,
@@ -1807,17 +1822,21 @@ void launch_armed_w(const ArmArgs& a, hipStream_t st) {
   // the wide kernel too (one CU per workgroup, up to 128 CUs).  Off by
   // default, as is PBFTV_QC_YIELD: a whole CU taken from a concurrent batch
   // costs it 3-7 % (each XCD's share waits for its slowest CU).
+  // (experiments) a number k >= 2: the narrow row kernel's workgroups take k
+  // KiB of LDS, so a concurrent batch fits fewer blocks (39 KiB each) on
+  // their CUs -- a partial exclusivity
   const char* e = getenv("PBFTV_QC_EXCLUSIVE_CU");
   const bool wide = a.relay != nullptr;
   const bool excl = e && (e[0] == '1' || (!wide && e[0] == 'n'));
+  const uint32_t part_kb = e && !wide && e[0] >= '2' && e[0] <= '9' ? (uint32_t)atoi(e) : 0u;
   if constexpr (RowsGeom<WG, WQ>::ok) {
     if (rows_enabled()) {
-      const uint32_t rl = excl ? 160u * 1024u - 4096u : 0u;  // (+ the kernel's static LDS)
+      const uint32_t rl = excl ? 160u * 1024u - 4096u : part_kb ? std::min(part_kb, 156u) * 1024u : 0u;  // (+ static LDS)
       if (rl) {
         static bool rattr = false;
         if (!rattr) {
           (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ecdsa_rows_armed<WG, WQ>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)rl);
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160u * 1024u - 4096u));
           rattr = true;
         }
       }
@@ -1844,14 +1863,20 @@ template <int WG, int WQ>
 void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* key_idx, uint64_t n,
                           const uint32_t* key_valid, uint32_t nkeys, const uint32_t* gtab,
                           const uint32_t* const* qtabs,
-                          uint8_t* bitmap, uint8_t* okbytes, hipStream_t st) {
+                          uint8_t* bitmap, uint8_t* okbytes, hipStream_t st, bool one_wave = false) {
   if constexpr (RowsGeom<WG, WQ>::ok) {
-    if (n <= rows_max_batch() && rows_enabled()) {
+    if (n <= rows_max_batch() && rows_enabled() && !one_wave) {
       hipLaunchKernelGGL((k_ecdsa_rows<WG, WQ>), dim3((uint32_t)n), dim3(64 * RowsGeom<WG, WQ>::waves), 0, st, hashes, sigs, key_idx,
                          n, key_valid, nkeys, reinterpret_cast<const uint4*>(gtab),
                          reinterpret_cast<const uint4* const*>(qtabs), bitmap, okbytes);
       return;
     }
+  }
+  if (one_wave) {
+    hipLaunchKernelGGL((k_ecdsa_wave_lean<WG, WQ>), dim3((uint32_t)n), dim3(64), 0, st, hashes, sigs, key_idx, n,
+                       key_valid, nkeys, reinterpret_cast<const uint4*>(gtab),
+                       reinterpret_cast<const uint4* const*>(qtabs), bitmap, okbytes);
+    return;
   }
   hipLaunchKernelGGL((k_ecdsa_wave<WG, WQ>), dim3((uint32_t)n), dim3(64), 0, st, hashes, sigs, key_idx, n, key_valid,
                      nkeys, reinterpret_cast<const uint4*>(gtab), reinterpret_cast<const uint4* const*>(qtabs), bitmap,
@@ -1894,7 +1919,7 @@ void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint
 #define PBFTV_PART_WAVE_CASE(G, Q)                                                                            \
   if (wg == G && wq == Q) {                                                                                   \
     launch_wave_w<G, Q>(a.hashes, a.sigs, a.key_idx, a.n, a.key_valid, a.nkeys, a.gtab, a.qtabs, a.bitmap,    \
-                        a.okbytes, st);                                                                       \
+                        a.okbytes, st, a.one_wave);                                                           \
     return true;                                                                                              \
   }
 

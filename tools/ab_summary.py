@@ -42,7 +42,8 @@ def summarise(w, runs):
     if kind == "load":
         js = [r[-1] for r in runs]
         p = "  ".join(f"{k} {med([j[k]['p50'] for j in js]):.1f}" for k in
-                      ("idle_3sigs", "loaded_3sigs", "idle_67sigs", "loaded_67sigs"))
+                      ("idle_3sigs", "loaded_3sigs", "loaded_3sigs_every_100ms", "idle_67sigs", "loaded_67sigs")
+                      if k in js[0])
         rr = {k: round(med([j["stream_rate_ratio"][k] for j in js]), 3) for k in js[0]["stream_rate_ratio"]}
         return f"p50 us: {p}  stream ratio {rr}"
     if kind == "idle":
