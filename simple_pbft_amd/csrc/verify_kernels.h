@@ -1438,6 +1438,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_wave(const uint8_t* __restrict__ h
                                                    const uint32_t* __restrict__ key_valid, uint32_t nkeys,
                                                    const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
                                                    uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+  __builtin_amdgcn_s_setprio(3);  // a latency-path kernel: its waves issue ahead of a concurrent batch's
   const uint64_t i = blockIdx.x;
   const bool ok = wave_verify_sig<WG, WQ>(hashes, sigs, key_idx, i, key_valid, nkeys, gtab, qtabs);
   if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
@@ -1453,6 +1454,7 @@ k_ecdsa_wave_lean(const uint8_t* __restrict__ hashes, const uint8_t* __restrict_
                   const uint32_t* __restrict__ key_idx, uint64_t n, const uint32_t* __restrict__ key_valid,
                   uint32_t nkeys, const uint4* __restrict__ gtab, const uint4* const* __restrict__ qtabs,
                   uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
+  __builtin_amdgcn_s_setprio(3);  // (as k_ecdsa_wave: ahead of the batch it runs beside)
   const uint64_t i = blockIdx.x;
   const bool ok = wave_verify_sig<WG, WQ>(hashes, sigs, key_idx, i, key_valid, nkeys, gtab, qtabs);
   if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, okbytes);
@@ -1468,6 +1470,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows(const uint8_t* __
                                                                const uint4* const* __restrict__ qtabs,
                                                                uint8_t* __restrict__ bitmap, uint8_t* __restrict__ okbytes) {
   __shared__ RowsShared sh;
+  __builtin_amdgcn_s_setprio(3);  // (as k_ecdsa_wave)
   const uint64_t i = blockIdx.x;
   uint32_t e[8] = {}, r[8] = {}, s[8] = {};
   bool key_ok = false;
