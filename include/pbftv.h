@@ -122,7 +122,7 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
  *   PBFTV_QC_WIDE=0           never arm the 128-wave form;
  *   PBFTV_QC_YIELD            whether a lane-path batch halts the armed
  *                             kernel (certificates meanwhile are launched,
- *                             ~0.3 ms beside the batch instead of ~0.05 ms;
+ *                             ~0.1 ms beside the batch instead of ~0.04 ms;
  *                             the keeper re-arms after it): "1" always, "0"
  *                             never; unset (default) when no certificate
  *                             came for PBFTV_QC_YIELD_IDLE_MS (50 ms).  A
