@@ -446,9 +446,10 @@ uint32_t qc_spin() {
 // the largest recent wide certificate, 72 for 67 votes) 6-9 %
 // (tools/armed_tax.py, profiles/r06_armed_tax_*.json).  A yielding server is
 // halted by the batch enqueue (note_busy); a certificate in the meantime is
-// launched on the free armed stream (it waits for free wave slots beside the
-// batch, ~0.3 ms instead of ~0.05 ms), and the keeper arms again once the
-// queued batches are expected to be done.
+// launched on the free armed stream (one 128-VGPR wave per signature at
+// raised priority, k_ecdsa_wave_lean: ~0.1 ms beside the batch instead of
+// ~0.04 ms), and the keeper arms again once the queued batches are expected
+// to be done.
 //   "1": always yield;  "0": never (a server stays resident beside batches);
 //   unset (the default): yield while certificates are sparse -- when none has
 //   come for PBFTV_QC_YIELD_IDLE_MS (default 50 ms).  A node whose
