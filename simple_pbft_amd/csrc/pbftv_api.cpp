@@ -407,11 +407,6 @@ bool qc_arm_enabled() {
   return e ? e[0] == '1' : true;
 }
 
-bool env_flag_default(const char* name, bool dflt) {
-  const char* e = getenv(name);
-  return e ? e[0] == '1' : dflt;
-}
-
 double env_ms(const char* name, double dflt) {
   const char* e = getenv(name);
   return e ? atof(e) : dflt;
@@ -2137,7 +2132,9 @@ int pbftv_ecdsa_p256_verify_batch(pbftv_ctx* ctx, const uint8_t* hashes, const u
       HIP_TRY(latency_stream(d, &lst));
       // beside this device's lane batches: one wave per signature (a row
       // workgroup would wait for several freed wave slots on one CU)
-      const bool one_wave = lane_busy(d) && env_flag_default("PBFTV_QC_BUSY_ONE_WAVE", true);
+      // (PBFTV_QC_BUSY_ONE_WAVE=0: never; =2: always -- tests of the one-wave kernel)
+      const char* ow = getenv("PBFTV_QC_BUSY_ONE_WAVE");
+      const bool one_wave = ow && ow[0] == '2' ? true : lane_busy(d) && !(ow && ow[0] == '0');
       HIP_TRY(timed(d, PBFTV_K_ECDSA_WAVE, lst, [&] {
         return pbftv::launch_ecdsa_wave(d.gbits, d.qbits, hp, sp, kp, n - lo, d.key_valid.as<uint32_t>(), d.nkeys,
                                         d.gtab->as<uint32_t>(), d.qptrs.as<const uint32_t* const>(), nullptr,

@@ -164,3 +164,33 @@ def test_row_tree_exceptional_paths(gq, ecdsa_fixtures, monkeypatch):
                     "launches": 1 if exc else 0}
             assert d == want, (a, d, want)
         assert v.qc_counters(0)["armed_wide"]
+
+
+@pytest.mark.parametrize("kernel", ["one_wave", "quad"])
+def test_row_tree_vectors_through_the_one_wave_kernels(kernel, ecdsa_fixtures, monkeypatch):
+    """The same vectors (and the golden ones, and conftest's crafted sums)
+    through the launched ONE-wave kernels, whose sums are grouped otherwise:
+    "one_wave" is k_ecdsa_wave_lean (128 VGPRs, what a certificate launched
+    beside a batch gets; PBFTV_QC_BUSY_ONE_WAVE=2 forces it), "quad" the quad
+    schedule's k_ecdsa_wave (PBFTV_QC_ROWS=0).  Every bit against the oracle's
+    expectation."""
+    from conftest import crafted_exceptional
+    from simple_pbft_amd import Verifier
+    gq = (29, 21)
+    monkeypatch.setenv("PBFTV_GBITS", str(gq[0]))
+    monkeypatch.setenv("PBFTV_QBITS", str(gq[1]))
+    monkeypatch.setenv("PBFTV_QC_ARM", "0")
+    if kernel == "one_wave":
+        monkeypatch.setenv("PBFTV_QC_BUSY_ONE_WAVE", "2")
+    else:
+        monkeypatch.setenv("PBFTV_QC_ROWS", "0")
+    keys, crafted, golden = _all_rows(gq, ecdsa_fixtures)
+    _, H2, S2, K2, E2 = crafted_exceptional()
+    extra = [(H2[i], S2[i], 0, bool(E2[i]), None, f"crafted {i}") for i in range(len(K2))]
+    allrows = crafted + golden + extra
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        assert v.table_config()[:2] == gq
+        for a in range(0, len(allrows), 100):
+            d, _ = _call(v, [r if r[4] is not None else r[:4] + (False,) + r[5:] for r in allrows[a:a + 100]])
+            assert d["launches"] == 1 and d["armed"] == 0 and d["exact_sigs"] == 0, d
