@@ -1046,7 +1046,7 @@ SHA_OPS_PER_BLOCK = 1528
 VALU_PEAK = 256 * 4 * 32 * 2.4e9   # full-rate 32-bit VALU: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
 
 
-PMC_JSON = os.path.join(ROOT, "profiles", "r05_final_pmc.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "r06_final_pmc.json")
 
 
 def pmc_figures(kernel: str, geometry):
