@@ -725,98 +725,145 @@ __device__ __forceinline__ int32_t lane_from_prev(int32_t x) {  // lane j <- lan
 __device__ __forceinline__ int32_t center30(uint32_t x) { return (int32_t)(x << 2) >> 2; }
 
 // divsteps30_var (safegcd.h) shaped for the scalar unit, where every
-// instruction of the one wave costs an issue slot (a lone wave issues one
-// instruction per ~4 cycles, so the inversion's latency is its instruction
-// count): -f^-1 mod 64 is recomputed only when f changes (a swap).
+// instruction of the one wave costs an issue slot: a lone wave issues one
+// scalar instruction per ~4.2 cycles and a conditional branch, taken or not,
+// costs ~24 (tools/divstep_lat.hip, profiles/r06_divstep_lat.json), so the
+// inversion's latency is its instruction count plus its branches.
 //
 // Hand-scheduled SALU (PBFTV_DIVSTEP_ASM, the default; the C++ form below is
-// the reference and the fallback): per elimination step 24 instructions
-// (the compiler's form: ~32, five of them register moves the swap's phi
-// nodes forced on the no-swap path).  The swap moves no register: the loop
-// exists twice, with (f, g), (u, q), (v, r) in exchanged registers, and a
-// swap negates three registers in place and continues in the other copy.
-//   z = min(ctz(g), i)             s_ff1 (-1 for g == 0) + s_min_u32
-//   w = (g nfi) & bfm(min(eta + 1, i, 6))   (the same mask as the C++ form)
+// the reference and the fallback), per common elimination step (a swap: 134
+// of ~141 per inversion) 24 instructions and ONE branch:
+//   STEP  z = min(ctz(g), i) (s_ff1 gives -1 for g == 0); the s_min's SCC is
+//         "ctz(g) < i" (the batch goes on), an s_cselect keeps e1 = eta + 1
+//         then and 0xFFFFFFFF otherwise, and after the shifts SCC = (that <= z)
+//         is "goes on AND swaps" -- the only branch.  Anything else (the
+//         batch's end, a step without a swap, a batch's first step with
+//         e1 < 0) takes the rare path, which tests exactly.
+//   SWAP  no register moves and no negations: the registers hold the f row
+//         (f, u, v) times s_f and the g row (g, q, r) times s_g, and the swap
+//         (f, g, u, v, q, r) <- (g, -f, q, r, -u, -v) exchanges the register
+//         roles (copy A <-> B) and turns (s_f, s_g) into (s_g, -s_f).  Four
+//         states S0 = A(+,+), S1 = B(+,-), S2 = A(-,-), S3 = B(-,+), one copy
+//         of the step each, fall through S0 -> S1 -> S2 -> S3, back edge to
+//         S0's swap.  What a swap still does: e1 <- 2 - e1 and nfi.
+//   ELIM  w = (g nfi) & bfm(min(e1, i, 6)), g += s w, q += s u w, r += s v w
+//         with s = s_f s_g (s_add or s_sub by state) and nfi = s (-f^-1 mod
+//         64) from the Newton step f (f f - 2) (or f (2 - f f)).
+// The exit block of each state restores the signs and the registers.
+// 141 steps: 22.4k cycles -> ~19.2k; the whole inversion 30.5k -> 25.4k with
+// inv_mod_n_wave's leaner batch below (bit-identical D over 256 inputs).
 // Scalar ALU only: no scalar memory access of any kind.
 #ifndef PBFTV_DIVSTEP_ASM
 #define PBFTV_DIVSTEP_ASM 1
 #endif
 #if PBFTV_DIVSTEP_ASM
-#define PBFTV_DS_STEP(F, G, U, V, Q, R, EXIT)                                                            \
-  "s_ff1_i32_b32 %[z], " G "\n"                                                                          \
-  "s_min_u32 %[z], %[z], %[i]\n"                                                                         \
-  "s_lshr_b32 " G ", " G ", %[z]\n"                                                                      \
-  "s_lshl_b32 " U ", " U ", %[z]\n"                                                                      \
-  "s_lshl_b32 " V ", " V ", %[z]\n"                                                                      \
-  "s_sub_i32 %[eta], %[eta], %[z]\n"                                                                     \
-  "s_sub_u32 %[i], %[i], %[z]\n"                                                                         \
-  "s_cmp_eq_u32 %[i], 0\n"                                                                               \
-  "s_cbranch_scc1 " EXIT "\n"
-#define PBFTV_DS_ELIM(F, G, U, V, Q, R)                                                                  \
-  "s_add_i32 %[m], %[eta], 1\n"                                                                          \
-  "s_min_u32 %[m], %[m], %[i]\n"                                                                         \
-  "s_min_u32 %[m], %[m], 6\n"                                                                            \
-  "s_bfm_b32 %[m], %[m], 0\n"                                                                            \
-  "s_mul_i32 %[w], " G ", %[nfi]\n"                                                                      \
-  "s_and_b32 %[w], %[w], %[m]\n"                                                                         \
-  "s_mul_i32 %[m], " F ", %[w]\n"                                                                        \
-  "s_add_u32 " G ", " G ", %[m]\n"                                                                       \
-  "s_mul_i32 %[m], " U ", %[w]\n"                                                                        \
-  "s_add_u32 " Q ", " Q ", %[m]\n"                                                                       \
-  "s_mul_i32 %[m], " V ", %[w]\n"                                                                        \
-  "s_add_u32 " R ", " R ", %[m]\n"
-// swap: (f, g, u, v, q, r, eta) <- (g, -f, q, r, -u, -v, -eta), in place: the
-// registers of f, u, v now hold -f, -u, -v = the new g, q, r
-#define PBFTV_DS_SWAP(F, G, U, V)                                                                        \
-  "s_sub_i32 %[eta], 0, %[eta]\n"                                                                        \
-  "s_sub_u32 " F ", 0, " F "\n"                                                                          \
-  "s_sub_u32 " U ", 0, " U "\n"                                                                          \
-  "s_sub_u32 " V ", 0, " V "\n"                                                                          \
-  "s_mul_i32 %[w], " G ", " G "\n"                                                                       \
-  "s_add_i32 %[w], %[w], -2\n"                                                                           \
-  "s_mul_i32 %[nfi], %[w], " G "\n"
+#define PBFTV_DS_STEP(G, U, V)                    \
+  "s_ff1_i32_b32 %[z], " G "\n"                   \
+  "s_min_u32 %[z], %[z], %[i]\n"                  \
+  "s_cselect_b32 %[k], %[e1], -1\n"               \
+  "s_lshr_b32 " G ", " G ", %[z]\n"               \
+  "s_lshl_b32 " U ", " U ", %[z]\n"               \
+  "s_lshl_b32 " V ", " V ", %[z]\n"               \
+  "s_sub_i32 %[e1], %[e1], %[z]\n"                \
+  "s_sub_u32 %[i], %[i], %[z]\n"                  \
+  "s_cmp_le_u32 %[k], %[z]\n"
+#define PBFTV_DS_SWAPIN(F, NFI)                   \
+  "s_sub_i32 %[e1], 2, %[e1]\n"                   \
+  "s_mul_i32 %[w], " F ", " F "\n"                \
+  NFI                                             \
+  "s_mul_i32 %[nfi], %[w], " F "\n"
+#define PBFTV_DS_NFI_POS "s_add_i32 %[w], %[w], -2\n"
+#define PBFTV_DS_NFI_NEG "s_sub_i32 %[w], 2, %[w]\n"
+#define PBFTV_DS_ELIM(F, G, U, V, Q, R, OP)       \
+  "s_mul_i32 %[w], " G ", %[nfi]\n"               \
+  "s_min_u32 %[m], %[e1], %[i]\n"                 \
+  "s_min_u32 %[m], %[m], 6\n"                     \
+  "s_bfm_b32 %[m], %[m], 0\n"                     \
+  "s_and_b32 %[w], %[w], %[m]\n"                  \
+  "s_mul_i32 %[m], " F ", %[w]\n"                 \
+  "s_mul_i32 %[t2], " U ", %[w]\n"                \
+  "s_mul_i32 %[t3], " V ", %[w]\n"                \
+  OP " " G ", " G ", %[m]\n"                      \
+  OP " " Q ", " Q ", %[t2]\n"                     \
+  OP " " R ", " R ", %[t3]\n"
+#define PBFTV_DS_ELIM_(...) PBFTV_DS_ELIM(__VA_ARGS__)
+// register roles: copy A = (f, g, u, v, q, r), copy B = (g, f, q, r, u, v)
+#define PBFTV_DS_A "%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]"
+#define PBFTV_DS_B "%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]"
+#define PBFTV_DS_RARE(K, NEXT, ELIM)              \
+  ".Lr" K "_%=:\n"                                \
+  "s_cmp_eq_u32 %[i], 0\n"                        \
+  "s_cbranch_scc1 .Lx" K "_%=\n"                  \
+  "s_cmp_lt_i32 %[e1], 1\n"                       \
+  "s_cbranch_scc1 .Ll" NEXT "_%=\n"               \
+  ELIM                                            \
+  "s_branch .Le" K "_%=\n"
 
 __device__ __forceinline__ int32_t divsteps30_scalar(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
-  uint32_t u = 1, v = 0, q = 0, r = 1, i = 30, z, w, m;
+  uint32_t u = 1, v = 0, q = 0, r = 1, i = 30, z, w, m, t2, t3, k;
+  uint32_t e1 = (uint32_t)(eta + 1);
   uint32_t nfi = f * (f * f - 2u);  // -f^-1 mod 64 (Newton step from f f = 1 mod 8)
-  // copy A: (f, g, u, v, q, r) in their own registers; copy B: exchanged
   asm volatile(
-      "s_branch .LdsA1_%=\n"
-      ".LdsA3_%=:\n" PBFTV_DS_ELIM("%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]")
-      ".LdsA1_%=:\n" PBFTV_DS_STEP("%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]", ".LdsXA_%=")
-      "s_cmp_lt_i32 %[eta], 0\n"
-      "s_cbranch_scc0 .LdsA3_%=\n"
-      PBFTV_DS_SWAP("%[f]", "%[g]", "%[u]", "%[v]")
-      ".LdsB3_%=:\n" PBFTV_DS_ELIM("%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]")
-      PBFTV_DS_STEP("%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]", ".LdsXB_%=")
-      "s_cmp_lt_i32 %[eta], 0\n"
-      "s_cbranch_scc0 .LdsB3_%=\n"
-      PBFTV_DS_SWAP("%[g]", "%[f]", "%[q]", "%[r]")
-      "s_branch .LdsA3_%=\n"
-      ".LdsXB_%=:\n"  // ended in copy B: back to copy A's registers
-      "s_mov_b32 %[w], %[f]\n"
-      "s_mov_b32 %[f], %[g]\n"
-      "s_mov_b32 %[g], %[w]\n"
+      PBFTV_DS_STEP("%[g]", "%[u]", "%[v]")  // entry: a step in S0
+      "s_cbranch_scc0 .Lr0_%=\n"
+      ".Ll1_%=:\n" PBFTV_DS_SWAPIN("%[g]", PBFTV_DS_NFI_NEG) PBFTV_DS_ELIM_(PBFTV_DS_B, "s_sub_u32")
+      ".Le1_%=:\n" PBFTV_DS_STEP("%[f]", "%[q]", "%[r]")
+      "s_cbranch_scc0 .Lr1_%=\n"
+      ".Ll2_%=:\n" PBFTV_DS_SWAPIN("%[f]", PBFTV_DS_NFI_POS) PBFTV_DS_ELIM_(PBFTV_DS_A, "s_add_u32")
+      ".Le2_%=:\n" PBFTV_DS_STEP("%[g]", "%[u]", "%[v]")
+      "s_cbranch_scc0 .Lr2_%=\n"
+      ".Ll3_%=:\n" PBFTV_DS_SWAPIN("%[g]", PBFTV_DS_NFI_NEG) PBFTV_DS_ELIM_(PBFTV_DS_B, "s_sub_u32")
+      ".Le3_%=:\n" PBFTV_DS_STEP("%[f]", "%[q]", "%[r]")
+      "s_cbranch_scc0 .Lr3_%=\n"
+      ".Ll0_%=:\n" PBFTV_DS_SWAPIN("%[f]", PBFTV_DS_NFI_POS) PBFTV_DS_ELIM_(PBFTV_DS_A, "s_add_u32")
+      ".Le0_%=:\n" PBFTV_DS_STEP("%[g]", "%[u]", "%[v]")
+      "s_cbranch_scc1 .Ll1_%=\n"
+      PBFTV_DS_RARE("0", "1", PBFTV_DS_ELIM_(PBFTV_DS_A, "s_add_u32"))
+      PBFTV_DS_RARE("1", "2", PBFTV_DS_ELIM_(PBFTV_DS_B, "s_sub_u32"))
+      PBFTV_DS_RARE("2", "3", PBFTV_DS_ELIM_(PBFTV_DS_A, "s_add_u32"))
+      PBFTV_DS_RARE("3", "0", PBFTV_DS_ELIM_(PBFTV_DS_B, "s_sub_u32"))
+      ".Lx1_%=:\n"  // ended in S1 = B(+,-): u = q', v = r', q = -u', r = -v'
       "s_mov_b32 %[w], %[u]\n"
       "s_mov_b32 %[u], %[q]\n"
-      "s_mov_b32 %[q], %[w]\n"
+      "s_sub_u32 %[q], 0, %[w]\n"
       "s_mov_b32 %[w], %[v]\n"
       "s_mov_b32 %[v], %[r]\n"
+      "s_sub_u32 %[r], 0, %[w]\n"
+      "s_branch .Lx0_%=\n"
+      ".Lx2_%=:\n"  // S2 = A(-,-)
+      "s_sub_u32 %[u], 0, %[u]\n"
+      "s_sub_u32 %[v], 0, %[v]\n"
+      "s_sub_u32 %[q], 0, %[q]\n"
+      "s_sub_u32 %[r], 0, %[r]\n"
+      "s_branch .Lx0_%=\n"
+      ".Lx3_%=:\n"  // S3 = B(-,+): u = -q', v = -r', q = u', r = v'
+      "s_mov_b32 %[w], %[u]\n"
+      "s_sub_u32 %[u], 0, %[q]\n"
+      "s_mov_b32 %[q], %[w]\n"
+      "s_mov_b32 %[w], %[v]\n"
+      "s_sub_u32 %[v], 0, %[r]\n"
       "s_mov_b32 %[r], %[w]\n"
-      ".LdsXA_%=:\n"
-      : [f] "+s"(f), [g] "+s"(g), [u] "+s"(u), [v] "+s"(v), [q] "+s"(q), [r] "+s"(r), [eta] "+s"(eta),
-        [i] "+s"(i), [nfi] "+s"(nfi), [z] "=&s"(z), [w] "=&s"(w), [m] "=&s"(m)
+      ".Lx0_%=:\n"
+      : [f] "+s"(f), [g] "+s"(g), [u] "+s"(u), [v] "+s"(v), [q] "+s"(q), [r] "+s"(r), [e1] "+s"(e1),
+        [i] "+s"(i), [nfi] "+s"(nfi), [z] "=&s"(z), [w] "=&s"(w), [m] "=&s"(m), [t2] "=&s"(t2), [t3] "=&s"(t3),
+        [k] "=&s"(k)
       :
       : "scc");
   t.u = (int32_t)u;
   t.v = (int32_t)v;
   t.q = (int32_t)q;
   t.r = (int32_t)r;
-  return eta;
+  return (int32_t)e1 - 1;
 }
 #undef PBFTV_DS_STEP
+#undef PBFTV_DS_SWAPIN
+#undef PBFTV_DS_NFI_POS
+#undef PBFTV_DS_NFI_NEG
 #undef PBFTV_DS_ELIM
-#undef PBFTV_DS_SWAP
+#undef PBFTV_DS_ELIM_
+#undef PBFTV_DS_A
+#undef PBFTV_DS_B
+#undef PBFTV_DS_RARE
 #else
 __device__ __forceinline__ int32_t divsteps30_scalar(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
   uint32_t u = 1, v = 0, q = 0, r = 1;
@@ -878,6 +925,25 @@ __device__ __forceinline__ uint32_t lane_limb(const uint32_t v[9], int L) {
   return r;
 }
 
+// One batch: 30 divsteps on the scalar unit, then the matrix update of
+// (f, g) and (d, e) one lane per limb; TEST: returns g != 0.  md n_L is one
+// signed 64-bit MAD (nl's sign hidden from the compiler, which would otherwise
+// split it into unsigned multiplies and a sign fix).
+template <bool TEST>
+__device__ __forceinline__ bool inv_batch(int32_t& A, int32_t& B, int32_t& eta, int32_t nl, bool top, int row) {
+  const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(B, 0);
+  const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane(A, 16), e0 = (uint32_t)__builtin_amdgcn_readlane(B, 16);
+  trans30 t;
+  eta = divsteps30_scalar(eta, f0, g0, t);
+  const int32_t md = center30(0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * kNInv30);
+  const int32_t me = center30(0u - ((uint32_t)t.q * d0 + (uint32_t)t.r * e0) * kNInv30);
+  const int64_t P = (int64_t)t.u * A + (int64_t)t.v * B + (int64_t)md * nl;
+  const int64_t Q = (int64_t)t.q * A + (int64_t)t.r * B + (int64_t)me * nl;
+  A = limbs_center(limbs_shift30(P), top);
+  B = limbs_center(limbs_shift30(Q), top);
+  return TEST ? __ballot(row == 0 && B != 0) != 0 : true;
+}
+
 // D = R x^-1 mod n + k n for some k >= 0 (D < 2^261, 29-bit limbs, uniform),
 // for 0 < x < n (uniform LE words).  Every lane of the wave must call it.
 __device__ __forceinline__ void inv_mod_n_wave(fe& D, const uint32_t x[8]) {
@@ -885,7 +951,8 @@ __device__ __forceinline__ void inv_mod_n_wave(fe& D, const uint32_t x[8]) {
   const bool act = L < 9 && row < 2, top = L == 8;
   s30 xs;
   words_to_s30(xs, x);
-  const uint32_t nl = act && row == 1 ? lane_limb(kN30, L) : 0u;
+  int32_t nl = act && row == 1 ? (int32_t)lane_limb(kN30, L) : 0;
+  asm volatile("" : "+v"(nl));
   int32_t A = act && row == 0 ? (int32_t)lane_limb(kN30, L) : 0;                         // f = n, d = 0
   const uint32_t xl = lane_limb(reinterpret_cast<const uint32_t*>(xs.v), L);
   const uint32_t rl = lane_limb(kRN30, L);  // R mod n = 2^261 mod n
@@ -893,21 +960,14 @@ __device__ __forceinline__ void inv_mod_n_wave(fe& D, const uint32_t x[8]) {
   A = limbs_center(A, top);
   B = limbs_center(B, top);
   int32_t eta = -1;
+  // every input takes >= 17 batches since f starts at n: the first 14 skip the
+  // g == 0 test (a batch with g = 0 leaves f and d unchanged), so each batch
+  // ends in one branch
 #pragma unroll 1
-  for (int it = 0; it < 25; ++it) {
-    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(B, 0);
-    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane(A, 16), e0 = (uint32_t)__builtin_amdgcn_readlane(B, 16);
-    trans30 t;
-    eta = divsteps30_scalar(eta, f0, g0, t);
-    const int32_t md = center30(0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * kNInv30);
-    const int32_t me = center30(0u - ((uint32_t)t.q * d0 + (uint32_t)t.r * e0) * kNInv30);
-    const int64_t P = (int64_t)t.u * A + (int64_t)t.v * B + (int64_t)md * (int32_t)nl;
-    const int64_t Q = (int64_t)t.q * A + (int64_t)t.r * B + (int64_t)me * (int32_t)nl;
-    A = limbs_center(limbs_shift30(P), top);
-    B = limbs_center(limbs_shift30(Q), top);
-    if (it >= 14 && __ballot(row == 0 && B != 0) == 0) break;  // g == 0: f = +-1, d = +-R x^-1 (tested from batch 15:
-    // every input takes >= 17 batches since f starts at n; a batch with g = 0 leaves f and d unchanged)
-  }
+  for (int it = 0; it < 14; ++it) inv_batch<false>(A, B, eta, nl, top, row);
+#pragma unroll 1
+  for (int it = 14; it < 25; ++it)
+    if (!inv_batch<true>(A, B, eta, nl, top, row)) break;  // g == 0: f = +-1, d = +-R x^-1
   uint32_t fl0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), fl1 = (uint32_t)__builtin_amdgcn_readlane(A, 1);
   const bool pos = fl0 + (fl1 << 30) == 1u;  // f = +-1: its value mod 2^32
   // D = +-d + 16 n > 0 (|d| < 13.5 n), normalised 30-bit limbs, then 29-bit limbs

@@ -1,0 +1,615 @@
+// divstep_lat.hip -- the latency path's s^-1 (inv_mod_n_wave: divsteps on the
+// scalar unit, matrix updates one lane per limb) on ONE wave, as a certificate
+// signature runs it: cycles per inversion for the product's divstep schedule
+// and for candidate schedules, the share of the divstep chain, and the
+// per-instruction cost of short scalar / vector chains on a lone wave.
+// Measurement tool for DESIGN.md §7.3 (not the product).
+//   make -C simple_pbft_amd && hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/divstep_lat.hip -o tools/divstep_lat
+#include "../simple_pbft_amd/csrc/verify_kernels.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace pbftv;
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+// ---- candidate divstep schedule (v1) -----------------------------------------
+// As divsteps30_scalar, with e1 = eta + 1 kept instead of eta (the mask's
+// s_add goes; a swap is e1 <- 2 - e1), the exit test folded into the SCC of
+// the s_min that bounds z (SCC = ctz(g) < i: continue), and the three products
+// of an elimination in separate registers.
+#define DS1_STEP(F, G, U, V, XS)                  \
+  "s_ff1_i32_b32 %[z], " G "\n"                   \
+  "s_min_u32 %[z], %[z], %[i]\n"                  \
+  "s_cbranch_scc0 " XS "\n"                       \
+  "s_lshr_b32 " G ", " G ", %[z]\n"               \
+  "s_lshl_b32 " U ", " U ", %[z]\n"               \
+  "s_lshl_b32 " V ", " V ", %[z]\n"               \
+  "s_sub_i32 %[e1], %[e1], %[z]\n"                \
+  "s_sub_u32 %[i], %[i], %[z]\n"
+#define DS1_ELIM(F, G, U, V, Q, R)                \
+  "s_mul_i32 %[w], " G ", %[nfi]\n"               \
+  "s_min_u32 %[m], %[e1], %[i]\n"                 \
+  "s_min_u32 %[m], %[m], 6\n"                     \
+  "s_bfm_b32 %[m], %[m], 0\n"                     \
+  "s_and_b32 %[w], %[w], %[m]\n"                  \
+  "s_mul_i32 %[m], " F ", %[w]\n"                 \
+  "s_mul_i32 %[t2], " U ", %[w]\n"                \
+  "s_mul_i32 %[t3], " V ", %[w]\n"                \
+  "s_add_u32 " G ", " G ", %[m]\n"                \
+  "s_add_u32 " Q ", " Q ", %[t2]\n"               \
+  "s_add_u32 " R ", " R ", %[t3]\n"
+#define DS1_SWAP(F, G, U, V)                      \
+  "s_sub_i32 %[e1], 2, %[e1]\n"                   \
+  "s_sub_u32 " F ", 0, " F "\n"                   \
+  "s_sub_u32 " U ", 0, " U "\n"                   \
+  "s_sub_u32 " V ", 0, " V "\n"                   \
+  "s_mul_i32 %[w], " G ", " G "\n"                \
+  "s_add_i32 %[w], %[w], -2\n"                    \
+  "s_mul_i32 %[nfi], %[w], " G "\n"
+
+__device__ __forceinline__ int32_t divsteps_v1(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1, i = 30, z, w, m, t2, t3;
+  uint32_t e1 = (uint32_t)(eta + 1);
+  uint32_t nfi = f * (f * f - 2u);
+  asm volatile(
+      "s_branch .LvA1_%=\n"
+      ".LvA3_%=:\n" DS1_ELIM("%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]")
+      ".LvA1_%=:\n" DS1_STEP("%[f]", "%[g]", "%[u]", "%[v]", ".LvXA_%=")
+      "s_cmp_lt_i32 %[e1], 1\n"
+      "s_cbranch_scc0 .LvA3_%=\n"
+      DS1_SWAP("%[f]", "%[g]", "%[u]", "%[v]")
+      ".LvB3_%=:\n" DS1_ELIM("%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]")
+      DS1_STEP("%[g]", "%[f]", "%[q]", "%[r]", ".LvXB_%=")
+      "s_cmp_lt_i32 %[e1], 1\n"
+      "s_cbranch_scc0 .LvB3_%=\n"
+      DS1_SWAP("%[g]", "%[f]", "%[q]", "%[r]")
+      "s_branch .LvA3_%=\n"
+      ".LvXB_%=:\n"  // last shift in copy B, then back to copy A's registers
+      "s_lshl_b32 %[q], %[q], %[z]\n"
+      "s_lshl_b32 %[r], %[r], %[z]\n"
+      "s_sub_i32 %[e1], %[e1], %[z]\n"
+      "s_mov_b32 %[w], %[f]\n"
+      "s_mov_b32 %[f], %[g]\n"
+      "s_mov_b32 %[g], %[w]\n"
+      "s_mov_b32 %[w], %[u]\n"
+      "s_mov_b32 %[u], %[q]\n"
+      "s_mov_b32 %[q], %[w]\n"
+      "s_mov_b32 %[w], %[v]\n"
+      "s_mov_b32 %[v], %[r]\n"
+      "s_mov_b32 %[r], %[w]\n"
+      "s_branch .LvX_%=\n"
+      ".LvXA_%=:\n"
+      "s_lshl_b32 %[u], %[u], %[z]\n"
+      "s_lshl_b32 %[v], %[v], %[z]\n"
+      "s_sub_i32 %[e1], %[e1], %[z]\n"
+      ".LvX_%=:\n"
+      : [f] "+s"(f), [g] "+s"(g), [u] "+s"(u), [v] "+s"(v), [q] "+s"(q), [r] "+s"(r), [e1] "+s"(e1),
+        [i] "+s"(i), [nfi] "+s"(nfi), [z] "=&s"(z), [w] "=&s"(w), [m] "=&s"(m), [t2] "=&s"(t2), [t3] "=&s"(t3)
+      :
+      : "scc");
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return (int32_t)e1 - 1;
+}
+
+// ---- candidate divstep schedule (v2): one branch per elimination step -----------
+// The product's loop pays two conditional branches per step (exit test, swap
+// test) and an unconditional one per two steps; a branch costs a lone wave
+// ~24 cycles where an ALU instruction costs ~4.  Here STEP folds both tests
+// into one SCC: the s_min that bounds z sets SCC = ctz(g) < i (continue), an
+// s_cselect keeps e1 (= eta + 1) when continuing and 0xFFFFFFFF otherwise, and
+// SCC = (that <= z) is "continue AND swap" (e1 >= 0 here except on a batch's
+// first step, whose SCC may then say rare wrongly -- the rare path re-tests
+// exactly).  Common steps alternate between the two register copies: copy B
+// falls through into copy A, copy A's branch is the loop's back edge.
+#define DS2_STEP(F, G, U, V)                      \
+  "s_ff1_i32_b32 %[z], " G "\n"                   \
+  "s_min_u32 %[z], %[z], %[i]\n"                  \
+  "s_cselect_b32 %[k], %[e1], -1\n"               \
+  "s_lshr_b32 " G ", " G ", %[z]\n"               \
+  "s_lshl_b32 " U ", " U ", %[z]\n"               \
+  "s_lshl_b32 " V ", " V ", %[z]\n"               \
+  "s_sub_i32 %[e1], %[e1], %[z]\n"                \
+  "s_sub_u32 %[i], %[i], %[z]\n"                  \
+  "s_cmp_le_u32 %[k], %[z]\n"
+
+__device__ __forceinline__ int32_t divsteps_v2(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1, i = 30, z, w, m, t2, t3, k;
+  uint32_t e1 = (uint32_t)(eta + 1);
+  uint32_t nfi = f * (f * f - 2u);
+  asm volatile(
+      DS2_STEP("%[f]", "%[g]", "%[u]", "%[v]")  // entry: a step in copy A
+      "s_cbranch_scc0 .LwRA_%=\n"
+      ".LwSA_%=:\n" DS1_SWAP("%[f]", "%[g]", "%[u]", "%[v]")
+      DS1_ELIM("%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]")
+      ".LwB1_%=:\n" DS2_STEP("%[g]", "%[f]", "%[q]", "%[r]")
+      "s_cbranch_scc0 .LwRB_%=\n"
+      ".LwSB_%=:\n" DS1_SWAP("%[g]", "%[f]", "%[q]", "%[r]")
+      DS1_ELIM("%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]")
+      ".LwA1_%=:\n" DS2_STEP("%[f]", "%[g]", "%[u]", "%[v]")
+      "s_cbranch_scc1 .LwSA_%=\n"
+      ".LwRA_%=:\n"  // copy A, rare: the batch is done, or no swap, or a first step
+      "s_cmp_eq_u32 %[i], 0\n"
+      "s_cbranch_scc1 .LwX_%=\n"
+      "s_cmp_lt_i32 %[e1], 1\n"
+      "s_cbranch_scc1 .LwSA_%=\n"
+      DS1_ELIM("%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]")
+      "s_branch .LwA1_%=\n"
+      ".LwRB_%=:\n"
+      "s_cmp_eq_u32 %[i], 0\n"
+      "s_cbranch_scc1 .LwXB_%=\n"
+      "s_cmp_lt_i32 %[e1], 1\n"
+      "s_cbranch_scc1 .LwSB_%=\n"
+      DS1_ELIM("%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]")
+      "s_branch .LwB1_%=\n"
+      ".LwXB_%=:\n"  // done in copy B: back to copy A's registers
+      "s_mov_b32 %[w], %[f]\n"
+      "s_mov_b32 %[f], %[g]\n"
+      "s_mov_b32 %[g], %[w]\n"
+      "s_mov_b32 %[w], %[u]\n"
+      "s_mov_b32 %[u], %[q]\n"
+      "s_mov_b32 %[q], %[w]\n"
+      "s_mov_b32 %[w], %[v]\n"
+      "s_mov_b32 %[v], %[r]\n"
+      "s_mov_b32 %[r], %[w]\n"
+      ".LwX_%=:\n"
+      : [f] "+s"(f), [g] "+s"(g), [u] "+s"(u), [v] "+s"(v), [q] "+s"(q), [r] "+s"(r), [e1] "+s"(e1),
+        [i] "+s"(i), [nfi] "+s"(nfi), [z] "=&s"(z), [w] "=&s"(w), [m] "=&s"(m), [t2] "=&s"(t2), [t3] "=&s"(t3),
+        [k] "=&s"(k)
+      :
+      : "scc");
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return (int32_t)e1 - 1;
+}
+
+// ---- candidate divstep schedule (v3): v2 without the swap's negations ----------
+// The registers hold the f row (f, u, v) times s_f and the g row (g, q, r)
+// times s_g; a swap (f, g, u, v, q, r) <- (g, -f, q, r, -u, -v) then moves no
+// register and negates none: it exchanges the register roles (copy A <-> B)
+// and turns (s_f, s_g) into (s_g, -s_f).  Four states S0 = A(+,+), S1 =
+// B(+,-), S2 = A(-,-), S3 = B(-,+), one loop copy each; with sigma = s_f s_g
+// the elimination adds (sigma = +1) or subtracts (-1) F w, and nfi holds
+// sigma * (-F^-1 mod 64).  The exit block of each state restores the signs.
+#define DS3_SWAPIN(F, NEG)                        \
+  "s_sub_i32 %[e1], 2, %[e1]\n"                   \
+  "s_mul_i32 %[w], " F ", " F "\n"                \
+  NEG                                             \
+  "s_mul_i32 %[nfi], %[w], " F "\n"
+#define DS3_NFI_POS "s_add_i32 %[w], %[w], -2\n"
+#define DS3_NFI_NEG "s_sub_i32 %[w], 2, %[w]\n"
+#define DS3_ELIM(F, G, U, V, Q, R, OP)            \
+  "s_mul_i32 %[w], " G ", %[nfi]\n"               \
+  "s_min_u32 %[m], %[e1], %[i]\n"                 \
+  "s_min_u32 %[m], %[m], 6\n"                     \
+  "s_bfm_b32 %[m], %[m], 0\n"                     \
+  "s_and_b32 %[w], %[w], %[m]\n"                  \
+  "s_mul_i32 %[m], " F ", %[w]\n"                 \
+  "s_mul_i32 %[t2], " U ", %[w]\n"                \
+  "s_mul_i32 %[t3], " V ", %[w]\n"                \
+  OP " " G ", " G ", %[m]\n"                      \
+  OP " " Q ", " Q ", %[t2]\n"                     \
+  OP " " R ", " R ", %[t3]\n"
+#define DS3_ELIM_(...) DS3_ELIM(__VA_ARGS__)
+// register roles: copy A = (f, g, u, v, q, r), copy B = (g, f, q, r, u, v)
+#define DS3_A "%[f]", "%[g]", "%[u]", "%[v]", "%[q]", "%[r]"
+#define DS3_B "%[g]", "%[f]", "%[q]", "%[r]", "%[u]", "%[v]"
+#define DS3_RARE(K, NEXT, ELIM)                   \
+  ".Lr" K "_%=:\n"                                \
+  "s_cmp_eq_u32 %[i], 0\n"                        \
+  "s_cbranch_scc1 .Lx" K "_%=\n"                  \
+  "s_cmp_lt_i32 %[e1], 1\n"                       \
+  "s_cbranch_scc1 .Ll" NEXT "_%=\n"               \
+  ELIM                                            \
+  "s_branch .Le" K "_%=\n"
+
+__device__ __forceinline__ int32_t divsteps_v3(int32_t eta, uint32_t f, uint32_t g, trans30& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1, i = 30, z, w, m, t2, t3, k;
+  uint32_t e1 = (uint32_t)(eta + 1);
+  uint32_t nfi = f * (f * f - 2u);
+  asm volatile(
+      DS2_STEP("%[f]", "%[g]", "%[u]", "%[v]")  // entry: a step in S0
+      "s_cbranch_scc0 .Lr0_%=\n"
+      ".Ll1_%=:\n" DS3_SWAPIN("%[g]", DS3_NFI_NEG) DS3_ELIM_(DS3_B, "s_sub_u32")
+      ".Le1_%=:\n" DS2_STEP("%[g]", "%[f]", "%[q]", "%[r]")
+      "s_cbranch_scc0 .Lr1_%=\n"
+      ".Ll2_%=:\n" DS3_SWAPIN("%[f]", DS3_NFI_POS) DS3_ELIM_(DS3_A, "s_add_u32")
+      ".Le2_%=:\n" DS2_STEP("%[f]", "%[g]", "%[u]", "%[v]")
+      "s_cbranch_scc0 .Lr2_%=\n"
+      ".Ll3_%=:\n" DS3_SWAPIN("%[g]", DS3_NFI_NEG) DS3_ELIM_(DS3_B, "s_sub_u32")
+      ".Le3_%=:\n" DS2_STEP("%[g]", "%[f]", "%[q]", "%[r]")
+      "s_cbranch_scc0 .Lr3_%=\n"
+      ".Ll0_%=:\n" DS3_SWAPIN("%[f]", DS3_NFI_POS) DS3_ELIM_(DS3_A, "s_add_u32")
+      ".Le0_%=:\n" DS2_STEP("%[f]", "%[g]", "%[u]", "%[v]")
+      "s_cbranch_scc1 .Ll1_%=\n"
+      DS3_RARE("0", "1", DS3_ELIM_(DS3_A, "s_add_u32"))
+      DS3_RARE("1", "2", DS3_ELIM_(DS3_B, "s_sub_u32"))
+      DS3_RARE("2", "3", DS3_ELIM_(DS3_A, "s_add_u32"))
+      DS3_RARE("3", "0", DS3_ELIM_(DS3_B, "s_sub_u32"))
+      ".Lx1_%=:\n"  // B(+,-): u = q', v = r', q = -u', r = -v'
+      "s_mov_b32 %[w], %[u]\n"
+      "s_mov_b32 %[u], %[q]\n"
+      "s_sub_u32 %[q], 0, %[w]\n"
+      "s_mov_b32 %[w], %[v]\n"
+      "s_mov_b32 %[v], %[r]\n"
+      "s_sub_u32 %[r], 0, %[w]\n"
+      "s_branch .Lx0_%=\n"
+      ".Lx2_%=:\n"  // A(-,-)
+      "s_sub_u32 %[u], 0, %[u]\n"
+      "s_sub_u32 %[v], 0, %[v]\n"
+      "s_sub_u32 %[q], 0, %[q]\n"
+      "s_sub_u32 %[r], 0, %[r]\n"
+      "s_branch .Lx0_%=\n"
+      ".Lx3_%=:\n"  // B(-,+): u = -q', v = -r', q = u', r = v'
+      "s_mov_b32 %[w], %[u]\n"
+      "s_sub_u32 %[u], 0, %[q]\n"
+      "s_mov_b32 %[q], %[w]\n"
+      "s_mov_b32 %[w], %[v]\n"
+      "s_sub_u32 %[v], 0, %[r]\n"
+      "s_mov_b32 %[r], %[w]\n"
+      ".Lx0_%=:\n"
+      : [f] "+s"(f), [g] "+s"(g), [u] "+s"(u), [v] "+s"(v), [q] "+s"(q), [r] "+s"(r), [e1] "+s"(e1),
+        [i] "+s"(i), [nfi] "+s"(nfi), [z] "=&s"(z), [w] "=&s"(w), [m] "=&s"(m), [t2] "=&s"(t2), [t3] "=&s"(t3),
+        [k] "=&s"(k)
+      :
+      : "scc");
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return (int32_t)e1 - 1;
+}
+
+// counting form (C++; the product's fallback loop) for the step statistics
+__device__ __forceinline__ int32_t divsteps_count(int32_t eta, uint32_t f, uint32_t g, trans30& t, uint32_t& steps,
+                                                  uint32_t& swaps) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t nfi = f * (f * f - 2u);
+  int i = 30;
+  int z = __builtin_ctz(g | (0xFFFFFFFFu << i));
+  for (;;) {
+    g >>= z;
+    u <<= z;
+    v <<= z;
+    eta -= z;
+    i -= z;
+    if (i == 0) break;
+    ++steps;
+    if (eta < 0) {
+      ++swaps;
+      eta = -eta;
+      const uint32_t x = f, y = u, w = v;
+      f = g;
+      g = 0u - x;
+      u = q;
+      q = 0u - y;
+      v = r;
+      r = 0u - w;
+      nfi = f * (f * f - 2u);
+    }
+    const int lim = min(eta + 1, i);
+    const uint32_t w = (g * nfi) & ((1u << lim) - 1u) & 63u;
+    g += f * w;
+    q += u * w;
+    r += v * w;
+    z = __builtin_ctz(g | (0xFFFFFFFFu << i));
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return eta;
+}
+
+struct Stats {
+  uint64_t ds_cycles;
+  uint32_t batches, steps, swaps;
+};
+
+// inv_mod_n_wave (verify_kernels.h) with the divstep schedule chosen by V
+// (0: the product's, 1: v1, 2: counting) and optional stamps around the chain
+template <int V, bool STAMP>
+__device__ __forceinline__ void inv_copy(fe& D, const uint32_t x[8], Stats& st) {
+  const int lane = (int)(threadIdx.x & 63u), L = lane & 15, row = lane >> 4;
+  const bool act = L < 9 && row < 2, top = L == 8;
+  s30 xs;
+  words_to_s30(xs, x);
+  const uint32_t nl = act && row == 1 ? lane_limb(kN30, L) : 0u;
+  int32_t A = act && row == 0 ? (int32_t)lane_limb(kN30, L) : 0;
+  const uint32_t xl = lane_limb(reinterpret_cast<const uint32_t*>(xs.v), L);
+  const uint32_t rl = lane_limb(kRN30, L);
+  int32_t B = act ? (int32_t)(row == 0 ? xl : rl) : 0;
+  A = limbs_center(A, top);
+  B = limbs_center(B, top);
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int it = 0; it < 25; ++it) {
+    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(B, 0);
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane(A, 16), e0 = (uint32_t)__builtin_amdgcn_readlane(B, 16);
+    trans30 t;
+    uint64_t c0 = 0;
+    if constexpr (STAMP) c0 = __builtin_readcyclecounter();
+    if constexpr (V == 1) eta = divsteps_v1(eta, f0, g0, t);
+    else if constexpr (V == 3) eta = divsteps_v2(eta, f0, g0, t);
+    else if constexpr (V == 2) eta = divsteps_count(eta, f0, g0, t, st.steps, st.swaps);
+    else eta = divsteps30_scalar(eta, f0, g0, t);
+    if constexpr (STAMP) {
+      asm volatile("" ::"s"(t.u), "s"(t.r));
+      st.ds_cycles += __builtin_readcyclecounter() - c0;
+    }
+    ++st.batches;
+    const int32_t md = center30(0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * kNInv30);
+    const int32_t me = center30(0u - ((uint32_t)t.q * d0 + (uint32_t)t.r * e0) * kNInv30);
+    const int64_t P = (int64_t)t.u * A + (int64_t)t.v * B + (int64_t)md * (int32_t)nl;
+    const int64_t Q = (int64_t)t.q * A + (int64_t)t.r * B + (int64_t)me * (int32_t)nl;
+    A = limbs_center(limbs_shift30(P), top);
+    B = limbs_center(limbs_shift30(Q), top);
+    if (it >= 14 && __ballot(row == 0 && B != 0) == 0) break;
+  }
+  uint32_t fl0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), fl1 = (uint32_t)__builtin_amdgcn_readlane(A, 1);
+  const bool pos = fl0 + (fl1 << 30) == 1u;
+  uint32_t w30[9];
+  int64_t c = 0;
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) {
+    const int32_t dk = __builtin_amdgcn_readlane(A, 16 + k);
+    c += (int64_t)(pos ? dk : -dk) + 16 * (int64_t)kN30[k];
+    if (k < 8) {
+      w30[k] = (uint32_t)c & kM30;
+      c >>= 30;
+    } else {
+      w30[k] = (uint32_t)c;
+    }
+  }
+  PBFTV_UNROLL for (int j = 0; j < 9; ++j) {
+    const int bit = 29 * j, li = bit / 30, sh = bit % 30;
+    uint32_t v = w30[li] >> sh;
+    if (li + 1 < 9) v |= w30[li + 1] << (30 - sh);
+    D.v[j] = v & kMask29;
+  }
+}
+
+// v2 divsteps and a leaner batch: md n_L as one v_mad_i64_i32 (the compiler
+// splits it into unsigned multiplies when it can see n_L >= 0), and the loop
+// in two counted parts -- 14 batches without the g == 0 test (every input
+// takes >= 17), then the tested ones -- so each batch ends in one branch.
+template <bool TEST, int DS>
+__device__ __forceinline__ bool inv_batch_t(int32_t& A, int32_t& B, int32_t& eta, int32_t nl, bool top, int row) {
+  const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), g0 = (uint32_t)__builtin_amdgcn_readlane(B, 0);
+  const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane(A, 16), e0 = (uint32_t)__builtin_amdgcn_readlane(B, 16);
+  trans30 t;
+  eta = DS == 3 ? divsteps_v3(eta, f0, g0, t) : divsteps_v2(eta, f0, g0, t);
+  const int32_t md = center30(0u - ((uint32_t)t.u * d0 + (uint32_t)t.v * e0) * kNInv30);
+  const int32_t me = center30(0u - ((uint32_t)t.q * d0 + (uint32_t)t.r * e0) * kNInv30);
+  const int64_t P = (int64_t)t.u * A + (int64_t)t.v * B + (int64_t)md * nl;
+  const int64_t Q = (int64_t)t.q * A + (int64_t)t.r * B + (int64_t)me * nl;
+  A = limbs_center(limbs_shift30(P), top);
+  B = limbs_center(limbs_shift30(Q), top);
+  return TEST ? __ballot(row == 0 && B != 0) != 0 : true;
+}
+
+template <int DS>
+__device__ __forceinline__ void inv_v4(fe& D, const uint32_t x[8], Stats& st) {
+  const int lane = (int)(threadIdx.x & 63u), L = lane & 15, row = lane >> 4;
+  const bool act = L < 9 && row < 2, top = L == 8;
+  s30 xs;
+  words_to_s30(xs, x);
+  int32_t nl = act && row == 1 ? (int32_t)lane_limb(kN30, L) : 0;
+  asm volatile("" : "+v"(nl));  // its sign unknown to the compiler: one signed 64-bit MAD
+  int32_t A = act && row == 0 ? (int32_t)lane_limb(kN30, L) : 0;
+  const uint32_t xl = lane_limb(reinterpret_cast<const uint32_t*>(xs.v), L);
+  const uint32_t rl = lane_limb(kRN30, L);
+  int32_t B = act ? (int32_t)(row == 0 ? xl : rl) : 0;
+  A = limbs_center(A, top);
+  B = limbs_center(B, top);
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int it = 0; it < 14; ++it) inv_batch_t<false, DS>(A, B, eta, nl, top, row);
+#pragma unroll 1
+  for (int it = 14; it < 25; ++it)
+    if (!inv_batch_t<true, DS>(A, B, eta, nl, top, row)) break;
+  st.batches = 0;
+  uint32_t fl0 = (uint32_t)__builtin_amdgcn_readlane(A, 0), fl1 = (uint32_t)__builtin_amdgcn_readlane(A, 1);
+  const bool pos = fl0 + (fl1 << 30) == 1u;
+  uint32_t w30[9];
+  int64_t c = 0;
+  PBFTV_UNROLL for (int k = 0; k < 9; ++k) {
+    const int32_t dk = __builtin_amdgcn_readlane(A, 16 + k);
+    c += (int64_t)(pos ? dk : -dk) + 16 * (int64_t)kN30[k];
+    if (k < 8) {
+      w30[k] = (uint32_t)c & kM30;
+      c >>= 30;
+    } else {
+      w30[k] = (uint32_t)c;
+    }
+  }
+  PBFTV_UNROLL for (int j = 0; j < 9; ++j) {
+    const int bit = 29 * j, li = bit / 30, sh = bit % 30;
+    uint32_t v = w30[li] >> sh;
+    if (li + 1 < 9) v |= w30[li + 1] << (30 - sh);
+    D.v[j] = v & kMask29;
+  }
+}
+
+constexpr int kIn = 256;
+
+// one wave, kIn inversions one after the other; per inversion: wall ticks,
+// core cycles, the chain's cycles (STAMP) and the step statistics (V 2)
+template <int V, bool STAMP>
+__global__ void __launch_bounds__(64) k_inv(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                            uint64_t* __restrict__ tm) {
+  for (int k = 0; k < kIn; ++k) {
+    uint32_t x[8];
+    PBFTV_UNROLL for (int j = 0; j < 8; ++j) x[j] = __builtin_amdgcn_readfirstlane(in[8 * k + j]);
+    Stats st{0, 0, 0, 0};
+    fe D;
+    asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");
+    const uint64_t w0 = wall_clock64(), c0 = __builtin_readcyclecounter();
+    if constexpr (V == 0) {
+      if constexpr (STAMP) inv_copy<0, true>(D, x, st);
+      else inv_mod_n_wave(D, x);  // the product's function itself
+    } else if constexpr (V == 4) {
+      inv_v4<2>(D, x, st);
+    } else if constexpr (V == 5) {
+      inv_v4<3>(D, x, st);
+    } else {
+      inv_copy<V, STAMP>(D, x, st);
+    }
+    asm volatile("" ::"v"(D.v[0]), "v"(D.v[8]));
+    const uint64_t c1 = __builtin_readcyclecounter(), w1 = wall_clock64();
+    if (threadIdx.x == 0) {
+      tm[6 * k + 0] = w1 - w0;
+      tm[6 * k + 1] = c1 - c0;
+      tm[6 * k + 2] = st.ds_cycles;
+      tm[6 * k + 3] = st.batches;
+      tm[6 * k + 4] = st.steps;
+      tm[6 * k + 5] = st.swaps;
+    }
+    if (threadIdx.x < 9) out[9 * k + threadIdx.x] = D.v[threadIdx.x];
+  }
+}
+
+// SCC after s_min_u32 (the v1 exit test relies on SCC = S0 < S1)
+__global__ void k_scc(const uint32_t* __restrict__ a, uint32_t* __restrict__ out) {
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = __builtin_amdgcn_readfirstlane(a[2 * k]), y = __builtin_amdgcn_readfirstlane(a[2 * k + 1]);
+    uint32_t m, s;
+    asm volatile("s_min_u32 %0, %2, %3\n s_cselect_b32 %1, 1, 0" : "=s"(m), "=s"(s) : "s"(x), "s"(y) : "scc");
+    if (threadIdx.x == 0) {
+      out[2 * k] = m;
+      out[2 * k + 1] = s;
+    }
+  }
+}
+
+// chains of 256 instructions on a lone wave: cycles per instruction
+template <int K>
+__global__ void __launch_bounds__(64) k_chain(const uint32_t* __restrict__ in, uint64_t* __restrict__ tm) {
+  uint32_t a = __builtin_amdgcn_readfirstlane(in[0]), b = __builtin_amdgcn_readfirstlane(in[1]);
+  uint32_t c = a ^ 5u, d = b ^ 7u, e = a ^ 11u;
+  uint64_t acc = in[threadIdx.x & 7];
+  uint32_t va = in[threadIdx.x & 7];
+  asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");
+  const uint64_t c0 = __builtin_readcyclecounter();
+  if constexpr (K == 0) asm volatile(".rept 256\n s_add_u32 %0, %0, %1\n .endr" : "+s"(a) : "s"(b) : "scc");
+  if constexpr (K == 1) asm volatile(".rept 256\n s_mul_i32 %0, %0, %1\n .endr" : "+s"(a) : "s"(b));
+  if constexpr (K == 2)
+    asm volatile(".rept 64\n s_add_u32 %0, %0, %4\n s_add_u32 %1, %1, %4\n s_add_u32 %2, %2, %4\n s_add_u32 %3, %3, %4\n .endr"
+                 : "+s"(a), "+s"(c), "+s"(d), "+s"(e) : "s"(b) : "scc");
+  if constexpr (K == 3)
+    asm volatile(".rept 128\n s_ff1_i32_b32 %1, %0\n s_lshr_b32 %0, %0, %1\n .endr" : "+s"(a), "=&s"(c) :: "scc");
+  if constexpr (K == 4)
+    asm volatile(".rept 128\n s_min_u32 %0, %0, %1\n s_cbranch_scc0 1f\n 1:\n .endr" : "+s"(a) : "s"(b) : "scc");
+  if constexpr (K == 5) asm volatile(".rept 256\n s_nop 0\n .endr");
+  if constexpr (K == 6) asm volatile(".rept 256\n v_add_u32 %0, %0, %1\n .endr" : "+v"(va) : "s"(b));
+  if constexpr (K == 7)  // VALU -> readlane -> SALU -> VALU round trips
+    asm volatile(".rept 64\n v_add_u32 %0, %0, %1\n s_nop 4\n v_readlane_b32 %1, %0, 0\n .endr" : "+v"(va), "+s"(b));
+  if constexpr (K == 8)
+    asm volatile(".rept 256\n v_mad_i64_i32 %0, vcc, %1, %1, %0\n .endr" : "+v"(acc) : "v"(va) : "vcc");
+  const uint64_t c1 = __builtin_readcyclecounter();
+  if (threadIdx.x == 0) {
+    tm[0] = c1 - c0;
+    tm[1] = a ^ b ^ c ^ d ^ e ^ va ^ acc;
+  }
+}
+
+static const char* kChainNames[] = {"s_add dependent", "s_mul dependent", "s_add 4 independent", "s_ff1 + s_lshr",
+                                    "s_min + s_cbranch (not taken)", "s_nop 0", "v_add dependent",
+                                    "v_add + s_nop 4 + v_readlane", "v_mad_i64_i32 dependent"};
+
+template <int K>
+static void chain(const uint32_t* din, uint64_t* dtm) {
+  double best = 1e30;
+  for (int rep = 0; rep < 5; ++rep) {
+    hipLaunchKernelGGL(k_chain<K>, dim3(1), dim3(64), 0, 0, din, dtm);
+    CHECK(hipDeviceSynchronize());
+    uint64_t c;
+    CHECK(hipMemcpy(&c, dtm, 8, hipMemcpyDeviceToHost));
+    best = std::min(best, (double)c);
+  }
+  const int n = (K == 3 || K == 4) ? 128 : (K == 7 ? 64 : 256);
+  printf("  \"%s\": %.2f,\n", kChainNames[K], best / n);
+}
+
+template <int V, bool STAMP>
+static std::vector<uint32_t> inv(const char* name, const uint32_t* din, uint32_t* dout, uint64_t* dtm, int rate_khz) {
+  hipLaunchKernelGGL((k_inv<V, STAMP>), dim3(1), dim3(64), 0, 0, din, dout, dtm);
+  CHECK(hipDeviceSynchronize());
+  hipLaunchKernelGGL((k_inv<V, STAMP>), dim3(1), dim3(64), 0, 0, din, dout, dtm);
+  CHECK(hipDeviceSynchronize());
+  std::vector<uint64_t> tm(6 * kIn);
+  std::vector<uint32_t> D(9 * kIn);
+  CHECK(hipMemcpy(tm.data(), dtm, tm.size() * 8, hipMemcpyDeviceToHost));
+  CHECK(hipMemcpy(D.data(), dout, D.size() * 4, hipMemcpyDeviceToHost));
+  std::vector<double> us, cyc, dsc;
+  double b = 0, s = 0, w = 0;
+  for (int k = 0; k < kIn; ++k) {
+    us.push_back((double)tm[6 * k] * 1e3 / rate_khz);
+    cyc.push_back((double)tm[6 * k + 1]);
+    dsc.push_back((double)tm[6 * k + 2]);
+    b += tm[6 * k + 3];
+    s += tm[6 * k + 4];
+    w += tm[6 * k + 5];
+  }
+  auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+  printf("  \"%s\": {\"us_p50\": %.3f, \"cycles_p50\": %.0f, \"clock_mhz\": %.0f", name, med(us), med(cyc),
+         med(cyc) / med(us));
+  if (STAMP) printf(", \"divstep_chain_cycles_p50\": %.0f, \"batches_mean\": %.2f", med(dsc), b / kIn);
+  if (V == 2) printf(", \"steps_mean\": %.2f, \"swaps_mean\": %.2f", s / kIn, w / kIn);
+  printf("},\n");
+  return D;
+}
+
+int main() {
+  std::vector<uint32_t> h(8 * kIn);
+  uint32_t s = 4242;
+  for (auto& x : h) { s = s * 1664525u + 1013904223u; x = s ^ (s >> 13); }
+  for (int k = 0; k < kIn; ++k) h[8 * k + 7] &= 0x7FFFFFFF;  // < n
+  uint32_t *din, *dout;
+  uint64_t* dtm;
+  CHECK(hipMalloc(&din, h.size() * 4));
+  CHECK(hipMalloc(&dout, 9 * kIn * 4));
+  CHECK(hipMalloc(&dtm, 6 * kIn * 8 + 4096));
+  CHECK(hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  int rate_khz = 0;
+  CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
+  // SCC of s_min_u32 first: v1's loop exit depends on it
+  const uint32_t pairs[8] = {3, 5, 5, 3, 4, 4, 0xFFFFFFFFu, 7};
+  uint32_t* dp;
+  CHECK(hipMalloc(&dp, 64));
+  CHECK(hipMemcpy(dp, pairs, 32, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_scc, dim3(1), dim3(64), 0, 0, dp, dp + 8);
+  CHECK(hipDeviceSynchronize());
+  uint32_t sc[8];
+  CHECK(hipMemcpy(sc, dp + 8, 32, hipMemcpyDeviceToHost));
+  const bool scc_ok = sc[0] == 3 && sc[1] == 1 && sc[2] == 3 && sc[3] == 0 && sc[4] == 4 && sc[5] == 0 && sc[6] == 7 &&
+                      sc[7] == 0;
+  printf("{\n  \"s_min_u32 scc = s0 < s1\": %s,\n  \"cycles_per_instruction\": {\n", scc_ok ? "true" : "false");
+  chain<0>(din, dtm); chain<1>(din, dtm); chain<2>(din, dtm); chain<3>(din, dtm); chain<4>(din, dtm);
+  chain<5>(din, dtm); chain<6>(din, dtm); chain<7>(din, dtm); chain<8>(din, dtm);
+  printf("  \"end\": 0},\n  \"inversion\": {\n");
+  const auto d0 = inv<0, false>("product inv_mod_n_wave", din, dout, dtm, rate_khz);
+  inv<0, true>("product divsteps, stamped", din, dout, dtm, rate_khz);
+  const auto d2 = inv<2, false>("C++ divsteps (counting)", din, dout, dtm, rate_khz);
+  bool same1 = false;
+  if (scc_ok) {
+    const auto d1 = inv<1, false>("v1 divsteps", din, dout, dtm, rate_khz);
+    inv<1, true>("v1 divsteps, stamped", din, dout, dtm, rate_khz);
+    const auto d3 = inv<3, false>("v2 divsteps", din, dout, dtm, rate_khz);
+    inv<3, true>("v2 divsteps, stamped", din, dout, dtm, rate_khz);
+    const auto d4 = inv<4, false>("v2 divsteps + lean batch", din, dout, dtm, rate_khz);
+    const auto d5 = inv<5, false>("v3 divsteps + lean batch", din, dout, dtm, rate_khz);
+    same1 = d1 == d0 && d3 == d0 && d4 == d0 && d5 == d0;
+  }
+  printf("  \"end\": 0},\n  \"v1_v2_v3_match_product\": %s, \"counting_matches_product\": %s\n}\n", same1 ? "true" : "false",
+         d2 == d0 ? "true" : "false");
+  return 0;
+}
