@@ -34,7 +34,8 @@ def summarise(w, runs):
                 f"{[(j['config5']['check'], j['pbft_digests']['check']) for j in js]}")
     if kind == "qc":
         js = [r[-1] for r in runs]
-        return "  ".join(f"{k} p50 {med([j[k]['p50_us'] for j in js]):.2f} us" for k in js[0])
+        return "  ".join(f"{k} p50 {med([j[k]['p50_us'] for j in js]):.2f} us" for k in js[0]
+                         if isinstance(js[0][k], dict))
     if kind == "tick":
         js = [r[-1] for r in runs]
         keys = [k for k in js[0] if isinstance(js[0][k], dict) and "p50" in js[0][k]]
