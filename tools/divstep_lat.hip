@@ -521,6 +521,55 @@ __global__ void __launch_bounds__(64) k_chain(const uint32_t* __restrict__ in, u
   }
 }
 
+// the latency path's whole scalar stage (inversion + u1, u2, r R products into
+// LDS, verify_kernels.h wave_scalars_lds) and its product step alone
+template <int K>
+__global__ void __launch_bounds__(64) k_tail(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                             uint64_t* __restrict__ tm) {
+  __shared__ uint32_t lds[32];
+  for (int k = 0; k < kIn; ++k) {
+    uint32_t x[8], e[8], r[8];
+    PBFTV_UNROLL for (int j = 0; j < 8; ++j) {
+      x[j] = __builtin_amdgcn_readfirstlane(in[8 * k + j]);
+      e[j] = __builtin_amdgcn_readfirstlane(in[8 * ((k + 1) % kIn) + j]);
+      r[j] = __builtin_amdgcn_readfirstlane(in[8 * ((k + 2) % kIn) + j]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");
+    uint64_t c0, c1;
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(c0)::"memory");
+    asm volatile("" : "+s"(x[0]), "+s"(e[0]), "+s"(r[0]) : "s"(c0));  // the work starts after the stamp
+    if constexpr (K == 0) {
+      wave_scalars_lds(e, r, x, lds, lds + 8, lds + 16);
+    } else {
+      fe a, b, m, prod;
+      const int role = (int)(threadIdx.x & 3u);
+      fe_from_words(a, e);
+      fe_from_words(b, x);
+      fe_set(m, kN);
+      fmont_lane(prod, a, b, m, role < 2 ? kNPrime : 1u);
+      if (threadIdx.x < 9) lds[threadIdx.x] = prod.v[threadIdx.x];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(c1)::"memory");
+    if (threadIdx.x == 0) tm[6 * k + 1] = c1 - c0;
+    __syncthreads();
+    if (threadIdx.x < 25) out[25 * k + threadIdx.x] = lds[threadIdx.x];
+  }
+}
+
+template <int K>
+static void tail(const char* name, const uint32_t* din, uint32_t* dout, uint64_t* dtm) {
+  for (int rep = 0; rep < 2; ++rep) {
+    hipLaunchKernelGGL(k_tail<K>, dim3(1), dim3(64), 0, 0, din, dout, dtm);
+    CHECK(hipDeviceSynchronize());
+  }
+  std::vector<uint64_t> tm(6 * kIn);
+  CHECK(hipMemcpy(tm.data(), dtm, tm.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<double> c;
+  for (int k = 0; k < kIn; ++k) c.push_back((double)tm[6 * k + 1]);
+  std::sort(c.begin(), c.end());
+  printf("  \"%s\": {\"cycles_p50\": %.0f},\n", name, c[c.size() / 2]);
+}
+
 static const char* kChainNames[] = {"s_add dependent", "s_mul dependent", "s_add 4 independent", "s_ff1 + s_lshr",
                                     "s_min + s_cbranch (not taken)", "s_nop 0", "v_add dependent",
                                     "v_add + s_nop 4 + v_readlane", "v_mad_i64_i32 dependent"};
@@ -576,7 +625,7 @@ int main() {
   uint32_t *din, *dout;
   uint64_t* dtm;
   CHECK(hipMalloc(&din, h.size() * 4));
-  CHECK(hipMalloc(&dout, 9 * kIn * 4));
+  CHECK(hipMalloc(&dout, 25 * kIn * 4));  // k_tail writes 25 words per input
   CHECK(hipMalloc(&dtm, 6 * kIn * 8 + 4096));
   CHECK(hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   int rate_khz = 0;
@@ -609,6 +658,8 @@ int main() {
     const auto d5 = inv<5, false>("v3 divsteps + lean batch", din, dout, dtm, rate_khz);
     same1 = d1 == d0 && d3 == d0 && d4 == d0 && d5 == d0;
   }
+  tail<0>("wave_scalars_lds (inversion + products + LDS)", din, dout, dtm);
+  tail<1>("fmont_lane product step alone", din, dout, dtm);
   printf("  \"end\": 0},\n  \"v1_v2_v3_match_product\": %s, \"counting_matches_product\": %s\n}\n", same1 ? "true" : "false",
          d2 == d0 ? "true" : "false");
   return 0;
