@@ -128,6 +128,13 @@ int pbftv_stream_wait(pbftv_ctx* ctx, int dev, void* stream);
  *                             came for PBFTV_QC_YIELD_IDLE_MS (50 ms).  A
  *                             resident server costs a busy stream ~3 %
  *                             (narrow) to 6-9 % (wide, 67 votes);
+ *   PBFTV_QC_CU_YIELD         while an armed workgroup serves, the lane-path
+ *                             comb waves on its CU park at their next step
+ *                             (a per-CU flag word; at most 50 µs): "1" the
+ *                             default, "0" never, "2" also on the CU that
+ *                             shares its instruction cache.  3 signatures
+ *                             beside a 1M stream 40.0 -> 33.5 µs p50 at the
+ *                             same stream rate;
  *   PBFTV_QC_EXCLUSIVE_CU     armed workgroups take whole CUs, so a
  *                             concurrent batch does not share their SIMDs
  *                             (with PBFTV_QC_YIELD=0): "narrow" the narrow

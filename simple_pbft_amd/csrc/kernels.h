@@ -61,9 +61,12 @@ hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, cons
 // okb == nullptr: records in arrival order, LSB-first bitmap (ceil(n/8) B)
 // written directly; else one byte per signature at its batch index (okb, n B)
 // and launch_pack_bits builds the bitmap.
+// cuflag: the device's certificate flags (kCuFlagWords, zeroed; null: the
+// comb never yields to an armed certificate on its CU, verify_kernels.h)
 hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab,
                              const uint32_t* const* qtabs,
-                             uint8_t* bitmap, uint8_t* okb, hipStream_t st);
+                             uint8_t* bitmap, uint8_t* okb, const uint32_t* cuflag, hipStream_t st);
+constexpr uint32_t kCuFlagWords = 4096;  // one word per (XCC, SE, SH, CU)
 // stage 0 (optional): per-key totals for the key order (scratch:
 // key_sort_scratch_bytes = a header of key_sort_header_bytes, which must be
 // ZERO when the scratch is first used and is left zero by every batch).
@@ -88,6 +91,7 @@ struct CombArgs {
   const uint32_t* const* qtabs;
   uint8_t* bitmap;
   uint8_t* okb;
+  const uint32_t* cuflag;
 };
 struct WaveArgs {
   const uint8_t* hashes;
@@ -178,6 +182,8 @@ struct ArmArgs {
   uint32_t stamps;     // 1: each serving wave writes its GPU timestamps (pbftv_qc_stamps*; PBFTV_QC_STAMPS=1)
   int slot;            // its armed stream slot: the expired word and live words it writes (QcMail)
   uint32_t slots;      // narrow row-schedule kernel: signature slots armed (<= kQcSlots; one workgroup each)
+  uint32_t* cuflag;    // the device's certificate flags (null: none); a serving workgroup raises its CU's word
+  uint32_t cuyield;    // 2: also the word of the CU sharing its instruction cache
 };
 hipError_t launch_ecdsa_wave_armed(int wg, int wq, const ArmArgs& a, hipStream_t st);
 

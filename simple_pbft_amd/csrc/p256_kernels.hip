@@ -764,9 +764,9 @@ hipError_t launch_ecdsa_scalars(const uint8_t* hashes, const uint8_t* sigs, cons
 
 hipError_t launch_ecdsa_comb(int wg, int wq, const void* rec, uint64_t n, const uint32_t* gtab,
                              const uint32_t* const* qtabs,
-                             uint8_t* bitmap, uint8_t* okb, hipStream_t st) {
+                             uint8_t* bitmap, uint8_t* okb, const uint32_t* cuflag, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  const CombArgs a{rec, n, gtab, qtabs, bitmap, okb};
+  const CombArgs a{rec, n, gtab, qtabs, bitmap, okb, cuflag};
   if (launch_comb_part_g29(wg, wq, a, st) || launch_comb_part_g26(wg, wq, a, st) ||
       launch_comb_part_g24(wg, wq, a, st) || launch_comb_part_small(wg, wq, a, st))
     return hipGetLastError();

@@ -258,6 +258,8 @@ struct Device {
   // the armed kernels' streams, relay words and keeper thread
   hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: a rotation's successor spins beside its predecessor
   hipStream_t lstream = nullptr;  // launched latency-path kernels: never queued behind a batch on d.stream
+  DevBuf cuflag;                           // certificate flags per CU (kCuFlagWords; zeroed at the first arming)
+  std::atomic<uint32_t*> cuflag_ready{nullptr};  // cuflag once zeroed (read by batch launches without the lock)
   DevBuf qrelay;                           // the wide kernels' relay words, one 64-B line per qstream:
                                            // uncached device memory (read and written past the 8 XCDs' L2s, so
                                            // no cache maintenance: an agent-scope acquire per poll would
@@ -427,6 +429,14 @@ uint64_t qc_arm_budget(int dev) {
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
   return (uint64_t)(qc_arm_ms() * khz);
+}
+
+// Whether the comb waves on a CU park while an armed workgroup there serves a
+// certificate (PBFTV_QC_CU_YIELD: 1 the default, 0 never, 2 also on the CU
+// that shares its instruction cache; verify_kernels.h comb_park)
+uint32_t qc_cu_yield() {
+  const char* e = getenv("PBFTV_QC_CU_YIELD");
+  return e ? (uint32_t)atoi(e) : 1u;
 }
 
 // what the armed kernel does between polls (ArmArgs::spin; PBFTV_QC_SPIN)
@@ -699,6 +709,13 @@ hipError_t qc_arm(Device& d) {
   d.qc_wmax = 0;
   const uint32_t wslots = (re && re[0] == '0') ? kQcCap : d.qc_wslots;
   const char* se = getenv("PBFTV_QC_STAMPS");
+  const uint32_t cuyield = qc_cu_yield();
+  if (cuyield && !d.cuflag.p) {  // zeroed before any kernel reads or writes it
+    HIP_TRY_E(d.cuflag.ensure(4 * pbftv::kCuFlagWords));
+    HIP_TRY_E(hipMemsetAsync(d.cuflag.p, 0, 4 * pbftv::kCuFlagWords, d.qstream[slot]));
+    HIP_TRY_E(hipStreamSynchronize(d.qstream[slot]));
+    d.cuflag_ready.store(d.cuflag.as<uint32_t>(), std::memory_order_release);
+  }
   const ArmArgs a{qc_mail(d),
                   want,
                   qc_arm_budget(d.id),
@@ -711,7 +728,9 @@ hipError_t qc_arm(Device& d) {
                   relay,
                   se && se[0] == '1' ? 1u : 0u,
                   slot,
-                  relay ? wslots : slots};
+                  relay ? wslots : slots,
+                  cuyield ? d.cuflag.as<uint32_t>() : nullptr,
+                  cuyield};
   HIP_TRY_E(pbftv::launch_ecdsa_wave_armed(d.gbits, d.qbits, a, d.qstream[slot]));
   d.arm_seq = d.armed_first = want;
   d.arm_waves = relay ? wslots : slots;
@@ -1126,8 +1145,9 @@ void pbftv_close(pbftv_ctx* ctx) {
     d->vs.release();
     for (DevBuf* b : {&d->qptrs, &d->key_valid, &d->hashes, &d->sigs, &d->key_idx,
                       &d->bitmap, &d->data, &d->offsets, &d->lengths, &d->order,
-                      &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok})
+                      &d->order_scratch, &d->digests, &d->expected, &d->shabits, &d->arena, &d->msgok, &d->cuflag})
       b->release();  // explicit, with this device current (the destructors are a backstop)
+    d->cuflag_ready.store(nullptr);
     for (HostBuf* b : {&d->stage, &d->mstage, &d->mout, &d->sstage}) b->release();
     if (d->scratch_ev) (void)hipEventDestroy(d->scratch_ev);
     for (auto& kv : d->reader_ev) (void)hipEventDestroy(kv.second);
@@ -1923,7 +1943,13 @@ static int verify_on_device(Device& d, const uint8_t* d_hashes, const uint8_t* d
   HIP_TRY(timed(d, PBFTV_K_ECDSA_COMB, st, [&] {
     return pbftv::launch_ecdsa_comb(d.gbits, d.qbits, sc.rec.p, n, d.gtab->as<uint32_t>(),
                                     d.qptrs.as<const uint32_t* const>(), d_bitmap,
-                                    sorted ? sc.okb.as<uint8_t>() : nullptr, st);
+                                    sorted ? sc.okb.as<uint8_t>() : nullptr,
+                                    // (only while a server is armed: the comb's
+                                    // per-step read of its CU's word costs ~0.4 %)
+                                    qc_cu_yield() && d.arm_seq.load(std::memory_order_relaxed)
+                                        ? d.cuflag_ready.load(std::memory_order_acquire)
+                                        : nullptr,
+                                    st);
   }));
   if (sorted) HIP_TRY(pbftv::launch_pack_bits(sc.okb.as<uint8_t>(), n, d_bitmap, st));
   if (!own) HIP_TRY(scratch_release(d, st));

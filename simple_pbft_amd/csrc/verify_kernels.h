@@ -238,12 +238,38 @@ __device__ __forceinline__ void read_entry_lds(uint4 (*sent)[PBFTV_COMB_BLOCK], 
 }
 
 
+// ---- a certificate's CU, yielded by the batch waves beside it (round 6) ----
+// An armed workgroup shares its CU with comb waves of any batch in flight:
+// its issue priority (s_setprio 3) wins the arbitration but not the VALU
+// cycles a comb wave's 64-bit MADs already hold, nor the instruction cache.
+// While it serves, the armed workgroup raises its CU's word in a per-device
+// flag array (kernels.h kCuFlagWords; index from the hardware IDs: XCC, SE,
+// SH, CU), and a comb wave on that CU parks (s_sleep) at its next step
+// boundary until the word drops -- at most kCuParkTicks, so a word left set
+// cannot hold a batch.  Only the CUs that serve pay: ~20 µs of their comb
+// waves per certificate.
+constexpr uint64_t kCuParkTicks = 5000;  // wall clock (100 MHz): 50 µs
+__device__ __forceinline__ uint32_t cu_flag_index() {
+  uint32_t hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return ((xcc & 15u) << 8) | ((hw >> 8) & 0xFFu);  // CU_ID, SH_ID, SE_ID of this XCC
+}
+__device__ __forceinline__ void comb_park(const uint32_t* f) {
+  const uint64_t t0 = wall_clock64();
+  do {
+    __builtin_amdgcn_s_sleep(4);
+  } while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0 &&
+           wall_clock64() - t0 < kCuParkTicks);
+}
+
 template <int WG, int WQ>
 __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_comb(const SigRec* __restrict__ rec, uint64_t n,
                                                                     const uint4* __restrict__ gtab,
                                                                     const uint4* const* __restrict__ qtabs,
                                                                     uint8_t* __restrict__ bitmap,
-                                                                    uint8_t* __restrict__ okb) {
+                                                                    uint8_t* __restrict__ okb,
+                                                                    const uint32_t* __restrict__ cuflag) {
   using S = CombSteps<WG, WQ>;
   // signed digits of u1 / u2 in step order, one column per thread: recoded once
   // in the prologue so the main loop holds no 256-bit digit shift registers
@@ -325,17 +351,22 @@ __global__ void __launch_bounds__(PBFTV_COMB_BLOCK, PBFTV_COMB_WAVES) k_ecdsa_co
 #ifndef PBFTV_COMB_UNROLL
 #define PBFTV_COMB_UNROLL 1
 #endif
+  const uint32_t* cuf = cuflag ? cuflag + cu_flag_index() : nullptr;  // (uniform)
 #pragma unroll PBFTV_COMB_UNROLL
   for (int j = j0; j < jend; ++j) {
     uint32_t w16[16];
     read_entry_lds(sent, t, w16);
     const int dc = d;
+    // this CU's certificate word, read behind the step (issued before the
+    // entry loads, so its wait does not wait for them)
+    const uint32_t cf = cuf ? __hip_atomic_load(cuf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     if (j + 1 < S::nD) {  // next step's entry streams into LDS during this addition
       d = (int)sdig[j + 1][t] + 1;
       issue_entry_lds(sent, t, S::is_q(j + 1) ? entry_ptr<WQ>(qtab, S::win(j + 1), d)
                                               : entry_ptr<WG>(gtab, S::win(j + 1), d));
     }
     comb_step_s(R, inf, neg_y, dc, w16);
+    if (cuf && __builtin_amdgcn_readfirstlane(cf) != 0) comb_park(cuf);
   }
   if (act) {
     const uint4 e = rp->q[4], f = rp->q[5];
@@ -1655,6 +1686,9 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
   // ---- slot wave ----
   const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b));
   const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
+  // this CU's word in the yield flags (and its instruction-cache partner's: cuyield 2)
+  uint32_t* const cuf = a.cuflag ? a.cuflag + cu_flag_index() : nullptr;
+  uint32_t* const cuf2 = cuf && a.cuyield == 2 ? a.cuflag + (cu_flag_index() ^ 1u) : nullptr;
   for (;; ++want) {
     uint32_t v = 0;
     bool serve = false;
@@ -1758,6 +1792,9 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
   uint32_t last = 0;  // a helper's last relayed request (the relay starts at {0, 0}; numbers are never 0)
   const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(helper ? 0 : b));
   const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
+  // this CU's word in the yield flags (and its instruction-cache partner's: cuyield 2)
+  uint32_t* const cuf = a.cuflag ? a.cuflag + cu_flag_index() : nullptr;
+  uint32_t* const cuf2 = cuf && a.cuyield == 2 ? a.cuflag + (cu_flag_index() ^ 1u) : nullptr;
   for (;; ++want) {
     uint32_t e[8] = {}, r[8] = {}, s[8] = {};
     bool key_ok = false;
@@ -1850,7 +1887,15 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
     if (c == 0u) return;
     if (c == 2u) continue;
     __builtin_amdgcn_s_setprio(3);
+    if (cuf && threadIdx.x == 0) {  // the comb waves on this CU park while it serves
+      __hip_atomic_fetch_add(cuf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cuf2) __hip_atomic_fetch_add(cuf2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const int ok = block_verify_rows<WG, WQ, false>(e, r, s, key_ok, gtab, qtab, &sh);  // 2: the host reruns it
+    if (cuf && threadIdx.x == 0) {
+      __hip_atomic_fetch_sub(cuf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cuf2) __hip_atomic_fetch_sub(cuf2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (wv == 0 && lane == 0) {
       constexpr uint32_t cap = QcMail::kQcCap;
       if (a.stamps) {
@@ -1948,11 +1993,11 @@ void launch_wave_w(const uint8_t* hashes, const uint8_t* sigs, const uint32_t* k
 
 template <int WG, int WQ>
 void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint32_t* const* qtabs, uint8_t* bitmap,
-                   uint8_t* okb, hipStream_t st) {
+                   uint8_t* okb, const uint32_t* cuflag, hipStream_t st) {
   const uint64_t blocks = (n + PBFTV_COMB_BLOCK - 1) / PBFTV_COMB_BLOCK;
   hipLaunchKernelGGL((k_ecdsa_comb<WG, WQ>), dim3((uint32_t)blocks), dim3(PBFTV_COMB_BLOCK), 0, st,
                      reinterpret_cast<const SigRec*>(rec), n, reinterpret_cast<const uint4*>(gtab),
-                     reinterpret_cast<const uint4* const*>(qtabs), bitmap, okb);
+                     reinterpret_cast<const uint4* const*>(qtabs), bitmap, okb, cuflag);
 }
 
 // One instantiation unit: the dispatchers for the geometry pairs COMBOS(X).
@@ -1971,7 +2016,7 @@ void launch_comb_w(const void* rec, uint64_t n, const uint32_t* gtab, const uint
   }
 #define PBFTV_PART_COMB_CASE(G, Q)                                                                            \
   if (wg == G && wq == Q) {                                                                                   \
-    launch_comb_w<G, Q>(a.rec, a.n, a.gtab, a.qtabs, a.bitmap, a.okb, st);                                    \
+    launch_comb_w<G, Q>(a.rec, a.n, a.gtab, a.qtabs, a.bitmap, a.okb, a.cuflag, st);                                    \
     return true;                                                                                              \
   }
 #define PBFTV_PART_ARMED_CASE(G, Q)                                                                           \
