@@ -255,6 +255,14 @@ __device__ __forceinline__ uint32_t cu_flag_index() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   return ((xcc & 15u) << 8) | ((hw >> 8) & 0xFFu);  // CU_ID, SH_ID, SE_ID of this XCC
 }
+// the armed side: wave 0 raises its CU's word (and the partner's) as soon as
+// it has a signature to serve, and drops it after the verdict
+__device__ __forceinline__ void raise_cu_flags(uint32_t* f, uint32_t* f2) {
+  if (f && (threadIdx.x & 63u) == 0) {
+    __hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f2) __hip_atomic_fetch_add(f2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 __device__ __forceinline__ void comb_park(const uint32_t* f) {
   const uint64_t t0 = wall_clock64();
   do {
@@ -1832,6 +1840,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
           armed_key(__builtin_amdgcn_readlane(v, 24), nkeys, qt_lo, qt_hi, kv_lo, kv_hi, a.key_valid, qtabs, key_ok, qtab);
         }
       }
+      if (c == 1u) raise_cu_flags(cuf, cuf2);
       if (lane == 0) cmd = c;
     } else if (wv == 0) {
       uint32_t v = 0;
@@ -1879,6 +1888,7 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
           armed_key(k, nkeys, qt_lo, qt_hi, kv_lo, kv_hi, a.key_valid, qtabs, key_ok, qtab);
         }
       }
+      if (c == 1u) raise_cu_flags(cuf, cuf2);
       if (lane == 0) cmd = c;
     }
     __syncthreads();
@@ -1887,10 +1897,6 @@ __global__ void __launch_bounds__(64 * kRowWaves) k_ecdsa_rows_armed(ArmArgs a) 
     if (c == 0u) return;
     if (c == 2u) continue;
     __builtin_amdgcn_s_setprio(3);
-    if (cuf && threadIdx.x == 0) {  // the comb waves on this CU park while it serves
-      __hip_atomic_fetch_add(cuf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cuf2) __hip_atomic_fetch_add(cuf2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     const int ok = block_verify_rows<WG, WQ, false>(e, r, s, key_ok, gtab, qtab, &sh);  // 2: the host reruns it
     if (cuf && threadIdx.x == 0) {
       __hip_atomic_fetch_sub(cuf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
