@@ -683,6 +683,43 @@ def _read(path: str):
         return None
 
 
+def _cpulist(text: str) -> list:
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def pin_to_gpu_node(dev: int):
+    """Run this process on the CPUs of the NUMA node its GPU hangs off
+    (sysfs numa_node of the GPU's PCI device, intersected with the allowed
+    CPUs), as INTEGRATION.md §3 asks of a node's caller: on a two-socket host
+    a 67-vote certificate from the other socket takes ~36 instead of ~31 us
+    (profiles/r06_numa/summary.txt).  PBFTV_BENCH_PIN=0 leaves the affinity
+    alone.  Returns what was done (for the JSON line)."""
+    if os.environ.get("PBFTV_BENCH_PIN") == "0" or not hasattr(os, "sched_setaffinity"):
+        return {"pinned": False, "why": "PBFTV_BENCH_PIN=0" if hasattr(os, "sched_setaffinity") else "no affinity API"}
+    try:
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, dev) != 0:
+            return {"pinned": False, "why": "hipDeviceGetPCIBusId failed"}
+        bus = buf.value.decode().lower()
+        node = int(_read(f"/sys/bus/pci/devices/{bus}/numa_node") or -1)
+        if node < 0:
+            return {"pinned": False, "why": f"no NUMA node for {bus}"}
+        cpus = sorted(set(_cpulist(_read(f"/sys/devices/system/node/node{node}/cpulist") or "")) &
+                      os.sched_getaffinity(0))
+        if not cpus:
+            return {"pinned": False, "why": f"no allowed CPU on node {node}"}
+        os.sched_setaffinity(0, cpus)
+        return {"pinned": True, "numa_node": node, "cpus": len(cpus), "gpu_bus": bus}
+    except (OSError, ValueError) as e:
+        return {"pinned": False, "why": repr(e)}
+
+
 def cpu_allotment() -> dict:
     """The host CPUs this process may actually use, with the evidence: the
     scheduler affinity mask (os.sched_getaffinity), the cgroup-v2 CPU quota
@@ -1138,6 +1175,7 @@ def main():
     # one GPU per rank; PBFTV_BENCH_SHARE_DEVICE=1 puts every rank on device 0
     # (only to rehearse the N > 1 flow on a 1-GPU box -- not a scaling number)
     share = os.environ.get("PBFTV_BENCH_SHARE_DEVICE") == "1"
+    affinity = pin_to_gpu_node(0 if share else local)
     ver = Verifier(device_mask=1 if share else 1 << local)
     if ver.device_count() != 1 or (not share and ver.device_id(0) != local):
         raise SystemExit(f"bench.py rank {rank}: expected GPU {local}, the context has "
@@ -1267,6 +1305,7 @@ def main():
     }
     if one_stream_ms is not None:
         out["ms_per_step_one_stream"] = one_stream_ms
+    out["affinity"] = affinity
     if rank == 0:
         comb_avg = comb_ms / max(comb_cnt, 1) * 1e-3
         scal_avg = scal_ms / max(scal_cnt, 1) * 1e-3
