@@ -147,3 +147,21 @@ def test_bench_gpus_mismatch_fails_loudly():
     """Under torch.distributed.run with a world size other than --gpus, bench.py refuses."""
     r = _bench(["--gpus", "2", "--n", "4096"], {"WORLD_SIZE": "1"})
     assert r.returncode != 0 and "--gpus 2 but WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_numa_pinning_helpers(monkeypatch):
+    """bench.py pins each rank to its GPU's NUMA node:
+    the cpulist parser, the opt-out, and a graceful no-op where the GPU's
+    bus id or node cannot be read (this container has no GPU) -- the
+    affinity is left as it was."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench._cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert bench._cpulist("") == []
+    before = os.sched_getaffinity(0)
+    monkeypatch.setenv("PBFTV_BENCH_PIN", "0")
+    assert bench.pin_to_gpu_node(0) == {"pinned": False, "why": "PBFTV_BENCH_PIN=0"}
+    monkeypatch.delenv("PBFTV_BENCH_PIN")
+    r = bench.pin_to_gpu_node(0)
+    assert r["pinned"] is False and r["why"]
+    assert os.sched_getaffinity(0) == before
