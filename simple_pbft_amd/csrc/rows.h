@@ -25,15 +25,20 @@
 
 namespace pbftv {
 
+// (mov_dpp, not update_dpp with an old value of 0: every lane of these DPP
+// moves has a source lane or bound_ctrl's zero, so the old value is never
+// read, and without it the compiler drops the v_mov that materialised it --
+// two per product round, 324 instructions of the row kernel; QC p50 -0.5 µs,
+// profiles/r06_ab_mov_dpp)
 template <int K>
 __device__ __forceinline__ uint32_t row_bcast(uint32_t x) {  // lane K of the row to the whole row
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + K, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + K, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint32_t row_next(uint32_t x) {  // lane j <- lane j + 1 of its row (0 past it)
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, true);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x101, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t row_prev(uint32_t x) {  // lane j <- lane j - 1 of its row (0 before it)
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xF, 0xF, true);
 }
 
 // per-lane constants of the row layout

@@ -755,10 +755,10 @@ __device__ __forceinline__ bool wave_verify_quads(bool& exc, const uint32_t u1[8
 // emulates the scheme and checks every bound).  e starts at R mod n, so the
 // result is R s^-1 (Montgomery form for the u1 / u2 products, no extra one).
 __device__ __forceinline__ int32_t lane_from_next(int32_t x) {  // lane j <- lane j + 1 of its row (0 past the row)
-  return __builtin_amdgcn_update_dpp(0, x, 0x101, 0xF, 0xF, true);
+  return __builtin_amdgcn_mov_dpp(x, 0x101, 0xF, 0xF, true);
 }
 __device__ __forceinline__ int32_t lane_from_prev(int32_t x) {  // lane j <- lane j - 1 of its row (0 before it)
-  return __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);
+  return __builtin_amdgcn_mov_dpp(x, 0x111, 0xF, 0xF, true);
 }
 
 __device__ __forceinline__ int32_t center30(uint32_t x) { return (int32_t)(x << 2) >> 2; }
