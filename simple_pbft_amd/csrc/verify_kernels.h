@@ -1694,9 +1694,6 @@ __global__ void __launch_bounds__(256) k_ecdsa_wave_armed(ArmArgs a) {
   // ---- slot wave ----
   const uint32_t* slot = reinterpret_cast<const uint32_t*>(base + QcMail::slot_off(b));
   const uint32_t* word = lane < 48 ? slot + lane : reinterpret_cast<const uint32_t*>(base) + (lane - 48);
-  // this CU's word in the yield flags (and its instruction-cache partner's: cuyield 2)
-  uint32_t* const cuf = a.cuflag ? a.cuflag + cu_flag_index() : nullptr;
-  uint32_t* const cuf2 = cuf && a.cuyield == 2 ? a.cuflag + (cu_flag_index() ^ 1u) : nullptr;
   for (;; ++want) {
     uint32_t v = 0;
     bool serve = false;
