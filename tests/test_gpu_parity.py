@@ -1116,3 +1116,65 @@ def test_certificates_beside_a_batch(oracle_lib, mode, monkeypatch):
         finally:
             for b in (dh, ds, dk, db):
                 b.free()
+
+
+@pytest.mark.parametrize("cu_yield", ["1", "2"])
+def test_cu_yield_certificates_during_batches(oracle_lib, cu_yield, monkeypatch):
+    """The CU yield (PBFTV_QC_CU_YIELD; 2 also parks the instruction-cache
+    partner CU): with the narrow server held resident (PBFTV_QC_YIELD=0),
+    device-resident 1M batches on a library stream read their CU's certificate
+    word every comb step and park while an armed workgroup there serves.
+    Certificates served meanwhile by the armed server, and the batches' bitmap,
+    all against the oracle; the batches finish (a raised word parks a comb wave
+    at most 50 us)."""
+    import threading
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_YIELD", "0")
+    monkeypatch.setenv("PBFTV_QC_CU_YIELD", cu_yield)
+    monkeypatch.setenv("PBFTV_GBITS", "24")
+    monkeypatch.setenv("PBFTV_QBITS", "16")
+    keys, H, S, K = oracle_sign_pool(oracle_lib, 4, 16, seed=97)
+    S[::5, 9] ^= 0x08
+    n_all = len(K)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(H.ctypes.data, S.ctypes.data, K.ctypes.data, n_all, keys.ctypes.data,
+                                              len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+    n = 1 << 20
+    reps = n // n_all
+    with Verifier(device_mask=1) as v:
+        v.register_keys(keys)
+        dh, ds, dk = (v.to_device(0, np.tile(a, (reps, 1)) if a.ndim > 1 else np.tile(a, reps)) for a in (H, S, K))
+        db = v.alloc(0, n // 8 + 1)
+        st = v.stream_create(0)
+        try:
+            for i in range(0, 12, 3):  # arm the narrow server
+                assert (v.verify_batch(H[i:i + 3], S[i:i + 3], K[i:i + 3]) == want[i:i + 3]).all()
+            before = v.qc_counters(0)
+            stop = threading.Event()
+            done = [0]
+
+            def stream():
+                while not stop.is_set():
+                    v.verify_batch_dev(0, dh.ptr, ds.ptr, dk.ptr, n, db.ptr, stream=st)
+                    v.stream_wait(0, st)
+                    done[0] += 1
+            th = threading.Thread(target=stream)
+            th.start()
+            try:
+                calls = 0
+                while done[0] < 4 or calls < 40:
+                    i = 3 * (calls % (n_all // 3))
+                    assert (v.verify_batch(H[i:i + 3], S[i:i + 3], K[i:i + 3]) == want[i:i + 3]).all()
+                    calls += 1
+            finally:
+                stop.set()
+                th.join()
+            after = v.qc_counters(0)
+            assert after["armed"] - before["armed"] >= calls // 2  # served by the resident server
+            assert (np.unpackbits(db.to_host(), bitorder="little")[:n].astype(bool) == np.tile(want, reps)).all()
+        finally:
+            db.free()
+            v.stream_destroy(0, st)
+            for b in (dh, ds, dk):
+                b.free()
