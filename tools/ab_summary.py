@@ -35,7 +35,7 @@ def summarise(w, runs):
     if kind == "qc":
         js = [r[-1] for r in runs]
         return "  ".join(f"{k} p50 {med([j[k]['p50_us'] for j in js]):.2f} us" for k in js[0]
-                         if isinstance(js[0][k], dict))
+                         if isinstance(js[0][k], dict) and "p50_us" in js[0][k])
     if kind == "tick":
         js = [r[-1] for r in runs]
         keys = [k for k in js[0] if isinstance(js[0][k], dict) and "p50" in js[0][k]]

@@ -13,10 +13,12 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import synth  # noqa: E402
 from simple_pbft_amd import Verifier  # noqa: E402
+import bench  # noqa: E402
 from simple_pbft_amd.pbftv import K_ECDSA_WAVE  # noqa: E402
 
+pin = bench.pin_to_gpu_node(0)  # as bench.py: the 67-vote p50 follows the caller's socket
 ver = Verifier()
-out = {"lib": os.environ.get("PBFTV_LIB") or "base"}
+out = {"lib": os.environ.get("PBFTV_LIB") or "base", "affinity": pin}
 for n_keys, sigs in ((4, 3), (100, 67)):
     pub, H, S, K = synth.qc(n_keys, sigs, 5)
     ver.register_keys(pub)

@@ -17,6 +17,7 @@ from simple_pbft_amd import Verifier  # noqa: E402
 
 n = 1 << 20
 pub, H, S, K, ok = synth.config4(n, n_keys=100, seed=0x50424654)
+pin = bench.pin_to_gpu_node(0)  # as bench.py
 ver = Verifier(device_mask=1)
 ver.register_keys(pub)
 dh, ds, dk = ver.to_device(0, H), ver.to_device(0, S), ver.to_device(0, K)
