@@ -71,6 +71,15 @@ struct ArmRegistry {
   std::map<int, std::vector<pbftv::QcMail*>> mail;              // GPU -> registered mailboxes
   std::map<int, std::vector<std::condition_variable*>> keepers;  // GPU -> their devices' keeper wake-ups
   std::map<int, int> quiesce;                                   // GPU -> quiesces in progress
+  // The armed kernels' streams take high-priority hardware queues, and the
+  // runtime keeps only GPU_MAX_HW_QUEUES (4) of them per GPU: a fifth stream
+  // shares one, and a kernel launched there waits for the resident kernel's
+  // whole budget (tools/hiq_share.hip, profiles/r06_hiq_share.txt).  So the
+  // contexts of a process hold at most that many between them, a pair each
+  // (qc_streams_ready); a context without one launches its certificates on a
+  // normal-priority stream until a holder that has been idle gives its pair up.
+  std::map<int, int> hiq_pairs;                                           // GPU -> pairs held
+  std::map<int, std::chrono::steady_clock::time_point> hiq_wanted;       // GPU -> a context last found none free
 };
 ArmRegistry& arm_registry() {
   static ArmRegistry* r = new ArmRegistry;  // never destroyed: DevBuf destructors may run at exit
@@ -257,6 +266,7 @@ struct Device {
   VerifyScratch vs;  // the lane path's stage-1 records, prefix products, key order, result bytes
   // the armed kernels' streams, relay words and keeper thread
   hipStream_t qstream[2] = {nullptr, nullptr};  // alternate armings: a rotation's successor spins beside its predecessor
+  std::chrono::steady_clock::time_point qstream_given_up{};  // when this context last gave its pair to another (qc_streams_release)
   hipStream_t lstream = nullptr;  // launched latency-path kernels: never queued behind a batch on d.stream
   DevBuf cuflag;                           // certificate flags per CU (kCuFlagWords; zeroed at the first arming)
   std::atomic<uint32_t*> cuflag_ready{nullptr};  // cuflag once zeroed (read by batch launches without the lock)
@@ -600,16 +610,80 @@ void qc_keeper_loop(Device* d);
 // synchronous null-stream operation on the GPU (hipMemcpy, a caller's or this
 // library's) wait until it ends -- a full budget (tools/queue_share.hip,
 // profiles/r05_queue_share.txt).  The CP also dispatches them first.
+// Those queues are few (ArmRegistry::hiq_pairs): a context takes a pair only
+// while the process holds fewer than GPU_MAX_HW_QUEUES / 2 on the GPU;
+// otherwise it leaves qstream null (no armed server; latency_stream launches on
+// lstream) and asks the holders' keepers to give one up.
+int hiq_pair_cap() {
+  static const int cap = [] {
+    const char* e = getenv("GPU_MAX_HW_QUEUES");
+    const int q = e && atoi(e) > 0 ? atoi(e) : 4;
+    return std::max(1, q / 2);
+  }();
+  return cap;
+}
+
+// a context that found no pair free in the last second is waiting for one
+constexpr auto kHiqWantedFor = std::chrono::seconds(1);
+// a holder with no certificate for this long gives its pair to a waiting context
+constexpr auto kHiqIdleGiveUp = std::chrono::milliseconds(200);
+
 hipError_t qc_streams_ready(Device& d) {
+  if (d.qstream[0] && d.qstream[1]) return hipSuccess;
+  {
+    ArmRegistry& r = arm_registry();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (r.hiq_pairs[d.id] >= hiq_pair_cap()) {
+      r.hiq_wanted[d.id] = std::chrono::steady_clock::now();
+      for (std::condition_variable* cv : r.keepers[d.id]) cv->notify_one();  // (qc_keeper_loop)
+      return hipSuccess;
+    }
+    ++r.hiq_pairs[d.id];
+  }
   for (hipStream_t& q : d.qstream) {
-    if (q) continue;
     int lo = 0, hi = 0;
     const char* pe = getenv("PBFTV_QC_PRIO");  // (experiments) "0": normal-priority armed streams
+    hipError_t e = hipSuccess;
     if ((pe && pe[0] == '0') || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
         hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi) != hipSuccess)
-      HIP_TRY_E(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+      e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      for (hipStream_t& p : d.qstream)
+        if (p) {
+          (void)hipStreamDestroy(p);
+          p = nullptr;
+        }
+      ArmRegistry& r = arm_registry();
+      std::lock_guard<std::mutex> lk(r.mu);
+      --r.hiq_pairs[d.id];
+      return e;
+    }
   }
+  d.arm_stream = 1;  // (the first arming takes qstream[0])
   return hipSuccess;
+}
+
+// Give the pair back: the armed kernels leave first (qc_disarm), then the
+// streams go; the next call that arms claims a pair again.
+hipError_t qc_streams_release(Device& d) {
+  if (!d.qstream[0]) return hipSuccess;
+  HIP_TRY_E(qc_disarm(d));
+  for (hipStream_t& q : d.qstream) {
+    (void)hipStreamDestroy(q);
+    q = nullptr;
+  }
+  ArmRegistry& r = arm_registry();
+  std::lock_guard<std::mutex> lk(r.mu);
+  --r.hiq_pairs[d.id];
+  return hipSuccess;
+}
+
+// whether another context on this GPU asked for a pair lately
+bool hiq_wanted(const Device& d, std::chrono::steady_clock::time_point now) {
+  ArmRegistry& r = arm_registry();
+  std::lock_guard<std::mutex> lk(r.mu);
+  auto it = r.hiq_wanted.find(d.id);
+  return it != r.hiq_wanted.end() && now - it->second < kHiqWantedFor;
 }
 
 // Where a latency-path kernel is LAUNCHED (a certificate the armed server
@@ -618,14 +692,15 @@ hipError_t qc_streams_ready(Device& d) {
 // batch (a normal stream may share its hardware queue with the stream the
 // batches are queued on), dispatched first; the next arming queues behind the
 // short launched kernel.  While a rotation keeps both armed streams resident,
-// the normal-priority latency stream (lstream).  No extra high-priority
+// or while the context holds no pair (hiq_pair_cap), the normal-priority
+// latency stream (lstream).  No extra high-priority
 // stream: their hardware queues are few too, and a stream sharing one with a
 // resident armed kernel would wait for that kernel's budget.
 hipError_t latency_stream(Device& d, hipStream_t* out) {
   HIP_TRY_E(qc_streams_ready(d));
-  if (!d.arm_seq) {
+  if (d.qstream[0] && !d.arm_seq) {
     *out = d.qstream[0];
-  } else if (!d.retiring) {
+  } else if (d.qstream[0] && !d.retiring) {
     *out = d.qstream[d.arm_stream ^ 1];
   } else {
     if (!d.lstream) HIP_TRY_E(hipStreamCreateWithFlags(&d.lstream, hipStreamNonBlocking));
@@ -660,6 +735,7 @@ hipError_t qc_arm(Device& d) {
   if (qc_yield_now(d) && lane_busy(d)) return hipSuccess;  // the keeper arms once the batches are done
   HIP_TRY_E(qc_mail_ready(d));
   HIP_TRY_E(qc_streams_ready(d));
+  if (!d.qstream[0]) return hipSuccess;  // no high-priority pair free: certificates are launched
   uint32_t halt;
   {
     // the check and the halt snapshot in one critical section: a quiesce that
@@ -810,11 +886,24 @@ void qc_keeper_loop(Device* d) {
     const auto keep = std::chrono::microseconds((int64_t)(qc_keep_ms() * 1000.0));
     auto wake = now + far;
     qc_retire(*d);
+    // another context on this GPU is waiting for a high-priority pair
+    // (qc_streams_ready): ours goes to it once no certificate came here for
+    // kHiqIdleGiveUp; our next call claims one again
+    if (d->qstream[0] && hiq_wanted(*d, now)) {
+      if (now - d->last_qc >= kHiqIdleGiveUp) {
+        if (qc_streams_release(*d) != hipSuccess) (void)hipGetLastError();
+        d->qstream_given_up = now;
+      } else {
+        wake = d->last_qc + kHiqIdleGiveUp;
+      }
+    }
+    const bool given_up = !d->qstream[0] && d->last_qc <= d->qstream_given_up;  // (no call since: nothing to arm)
+    const bool wanted = !given_up && qc_arm_enabled() && d->have_keys && now - d->last_qc < keep;
     const int64_t busy_ns = d->busy_until_ns.load(std::memory_order_relaxed) - steady_ns();
-    if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep && qc_yield_now(*d) && busy_ns > 0) {
+    if (wanted && qc_yield_now(*d) && busy_ns > 0) {
       // lane-path batches are queued: nothing armed until they are expected done
-      wake = now + std::chrono::nanoseconds(busy_ns + 50000);
-    } else if (qc_arm_enabled() && d->have_keys && now - d->last_qc < keep) {
+      wake = std::min(wake, now + std::chrono::nanoseconds(busy_ns + 50000));
+    } else if (wanted) {
       // also re-arms after a disarm (key change) or a halt (quiesce)
       // (the kernel's SHAPE, narrow or wide, not its size: a wide arming takes
       // as many workgroups as the largest recent wide certificate)
@@ -824,7 +913,9 @@ void qc_keeper_loop(Device* d) {
         if (qc_rotate(*d) != hipSuccess) (void)hipGetLastError();  // a call will launch instead
         ++d->rotations;
       }
-      wake = d->arm_seq ? std::min(d->armed_at + half, d->last_qc + keep) : now + std::chrono::milliseconds(1);
+      wake = std::min(wake, d->arm_seq            ? std::min(d->armed_at + half, d->last_qc + keep)
+                            : d->qstream[0] ? now + std::chrono::milliseconds(1)
+                                            : now + std::chrono::milliseconds(50));  // (no pair free: retry)
     }
     if (d->retiring) wake = std::min(wake, now + std::chrono::microseconds(100));  // (a wide successor waits for its room)
     if (wake <= now) wake = now + std::chrono::milliseconds(1);
@@ -1134,8 +1225,7 @@ void pbftv_close(pbftv_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)qc_disarm(*d);  // the armed latency kernels exit before anything is freed
     qc_unregister(*d);
-    for (hipStream_t q : d->qstream)
-      if (q) (void)hipStreamDestroy(q);
+    (void)qc_streams_release(*d);
     (void)hipStreamSynchronize(d->stream);
     (void)collect_times(*d);
     for (auto& b : d->qblocks) b->release();

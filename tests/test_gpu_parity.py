@@ -750,19 +750,29 @@ def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypa
         for v in (a, b):
             for i in range(0, 12, 3):
                 call(v, i)
+            # (another context of this process -- the module's `ver` -- may hold
+            # a high-priority stream pair; it gives it up within ~0.2 s of idling)
+            t_end = time.perf_counter() + 3.0
+            while not call(v, 0) and time.perf_counter() < t_end:
+                time.sleep(0.01)
             assert call(v, 0)
         c0 = {id(v): v.qc_counters(0) for v in (a, b)}
-        for _ in range(20):
+        for it in range(20):
+            t0 = time.perf_counter()
             buf = a.alloc(0, 1 << 20)
+            assert time.perf_counter() - t0 < 0.05, ("alloc", it)
             t0 = time.perf_counter()
             buf.free()
-            assert time.perf_counter() - t0 < 0.05
+            assert time.perf_counter() - t0 < 0.05, ("free", it)
+            t0 = time.perf_counter()
             pin = a.pinned(np.zeros(1 << 16, np.uint8))
+            assert time.perf_counter() - t0 < 0.05, ("pinned", it)
             t0 = time.perf_counter()
             pin.free()
-            assert time.perf_counter() - t0 < 0.05
+            assert time.perf_counter() - t0 < 0.05, ("pinned free", it)
             for v in (a, b):  # served by the same armed servers, right after the frees
-                assert call(v, 12)
+                t0 = time.perf_counter()
+                assert call(v, 12), (it, v is a, time.perf_counter() - t0, v.qc_counters(0))
         for v in (a, b):
             c1 = v.qc_counters(0)
             assert c1["armed"] - c0[id(v)]["armed"] == 20 and c1["launches"] == c0[id(v)]["launches"], (c0[id(v)], c1)
@@ -772,6 +782,54 @@ def test_armed_kernel_does_not_hold_frees_or_other_contexts(oracle_lib, monkeypa
         assert call(a, 15)  # (a's server was not stopped by it)
         for i in range(24, n_all - 3, 3):
             for v in (a, b):
+                call(v, i)
+
+
+def test_armed_stream_pairs_shared_out(oracle_lib, monkeypatch):
+    """The runtime keeps GPU_MAX_HW_QUEUES (4) high-priority hardware queues
+    per GPU: a fifth high-priority stream shares one, and a kernel launched
+    there waits for the resident armed kernel's whole budget
+    (profiles/r06_hiq_share.txt; before the fix, a third armed context in one
+    process made certificates wait seconds).  Three contexts (beside the
+    module's) with 5-s budgets: no certificate waits, every bitmap is right,
+    at most GPU_MAX_HW_QUEUES / 2 contexts are armed at once, and the one that
+    keeps calling is served armed once the idle ones give a pair up."""
+    import os
+    import time
+    from simple_pbft_amd import Verifier
+    monkeypatch.setenv("PBFTV_QC_ARM_MS", "5000")
+    cap = max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) // 2)
+    keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=3, per_key=12, seed=83)
+    sigs[::4, 45] ^= 0x20
+    n_all = len(kidx)
+    want = np.zeros((n_all + 7) // 8, np.uint8)
+    oracle_lib.oracle_ecdsa_p256_verify_batch(hashes.ctypes.data, sigs.ctypes.data, kidx.ctypes.data, n_all,
+                                              keys.ctypes.data, len(keys), want.ctypes.data, 8)
+    want = np.unpackbits(want, bitorder="little")[:n_all].astype(bool)
+
+    def call(v, i):
+        t0 = time.perf_counter()
+        assert (v.verify_batch(hashes[i:i + 3], sigs[i:i + 3], kidx[i:i + 3]) == want[i:i + 3]).all(), i
+        dt = time.perf_counter() - t0
+        assert dt < 0.5, (i, dt)  # (a queue shared with a resident 5-s kernel: seconds)
+        return v.qc_stamps(0)["armed"]
+
+    with Verifier(device_mask=1) as a, Verifier(device_mask=1) as b, Verifier(device_mask=1) as c:
+        ctxs = (a, b, c)
+        for v in ctxs:
+            v.register_keys(keys)
+        for rnd in range(8):
+            for j, v in enumerate(ctxs):
+                call(v, 3 * ((rnd + j) % (n_all // 3)))
+            assert sum(v.qc_counters(0)["armed_waves"] > 0 for v in ctxs) <= cap
+        # a and b idle, c keeps calling: an idle holder gives its pair up
+        t_end = time.perf_counter() + 3.0
+        while not call(c, 0) and time.perf_counter() < t_end:
+            time.sleep(0.01)
+        assert call(c, 3)
+        assert sum(v.qc_counters(0)["armed_waves"] > 0 for v in ctxs) <= cap
+        for v in ctxs:  # every context still right, armed or launched
+            for i in range(0, n_all - 2, 3):
                 call(v, i)
 
 
