@@ -1,7 +1,8 @@
 """A bounded run of tools/stress.py inside the GPU suite:
 the standing check for the family of round 4's unexplained 0-of-67 false
 reject -- a key change, a free or a keeper rotation racing a certificate or a
-batch.  Two contexts on the GPU; worker threads submit certificates of 3 / 8 /
+batch.  Three contexts on the GPU (the third waits for a high-priority stream
+pair and takes one over when a holder idles); worker threads submit certificates of 3 / 8 /
 67 / 129 signatures (armed narrow, armed wide, launched), host-buffer and
 device-resident lane batches, while a control thread switches a context's
 whole key set, re-sets a key and frees device / pinned memory every 0.2-0.6 s
@@ -24,7 +25,8 @@ pytestmark = pytest.mark.gpu
 
 def test_stress_races_every_answer_checked():
     env = {k: v for k, v in os.environ.items() if not k.startswith("PBFTV_")}
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "stress.py"), "--seconds", "40"],
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "stress.py"), "--seconds", "40",
+                        "--contexts", "3"],
                        env=env, capture_output=True, text=True, timeout=200)
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert lines, (r.returncode, r.stderr[-3000:])
@@ -35,4 +37,6 @@ def test_stress_races_every_answer_checked():
     for k in ("cert3", "cert8", "cert67", "cert129", "host_batch", "dev_batch"):
         assert c.get(k, 0) >= 5, c
     assert c.get("ctl_switch", 0) + c.get("ctl_set_key", 0) >= 5 and c.get("ctl_dev_free", 0) >= 1, c
+    # the pairs changed hands: the contexts that idle now and then were served armed too
+    assert all(q["armed"] > 0 for q in out["qc_counters"]), out["qc_counters"]
     print(json.dumps({"stress": {"seconds": out["seconds"], "counts": c}}))

@@ -3,7 +3,11 @@ class of fault behind round 4's unexplained 0-of-67 --
 a key change, a free or a rotation racing a certificate -- looked for by
 running them all at once for a while.
 
-Two contexts on GPU 0.  Worker threads (each on its own context) submit, at
+Two contexts on GPU 0 (--contexts N: more; a third one finds the GPU's
+high-priority stream pairs taken and waits for an idle holder to hand one
+over, pbftv_api.cpp qc_streams_ready, so idle gaps are mixed in and pairs
+change hands while certificates race).  Worker threads (each on its own
+context) submit, at
 random: certificates of 3 / 8 / 67 / 129 signatures through pbftv_qc_verify
 (armed narrow / wide kernels, launches past 128), host-buffer lane batches,
 and device-resident batches on library streams.  A control thread every
@@ -126,7 +130,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--gbits", default="24")
     ap.add_argument("--qbits", default="16")
+    ap.add_argument("--contexts", type=int, default=2)
     a = ap.parse_args()
+    nctx = max(2, a.contexts)
     os.environ.setdefault("PBFTV_GBITS", a.gbits)
     os.environ.setdefault("PBFTV_QBITS", a.qbits)
     os.environ.setdefault("PBFTV_QC_ARM_MS", "30")
@@ -137,10 +143,10 @@ def main():
     L.oracle_ecdsa_p256_verify_batch.argtypes = [vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint32, vp, ctypes.c_int]
     rng = np.random.default_rng(20261018)
     sets = [make_set(synth, L, 0x50424654 + 17 * k, rng) for k in range(2)]
-    ctxs = [Verifier(device_mask=1) for _ in range(2)]
-    cur = [0, 1]  # key set of each context
-    locks = [RWLock() for _ in range(2)]  # workers shared; the control thread alone while it changes a context's keys
-    for c in range(2):
+    ctxs = [Verifier(device_mask=1) for _ in range(nctx)]
+    cur = [c % 2 for c in range(nctx)]  # key set of each context
+    locks = [RWLock() for _ in range(nctx)]  # workers shared; the control thread alone while it changes a context's keys
+    for c in range(nctx):
         ctxs[c].register_keys(sets[cur[c]][0])
     stop = threading.Event()
     counts, wrong, errors = {}, [], []
@@ -160,6 +166,10 @@ def main():
         try:
             while not stop.is_set():
                 kind = r.choice(kinds)
+                if kind == "idle":  # (a holder idle for 0.2 s hands its pair to a waiting context)
+                    time.sleep(r.uniform(0.1, 0.5))
+                    note(kind)
+                    continue
                 with locks[c].shared():
                     s = cur[c]
                     pub, certs, pool = sets[s]
@@ -209,7 +219,7 @@ def main():
             while not stop.is_set():
                 time.sleep(r.uniform(0.2, 0.6))
                 op = r.choice(["switch", "switch", "set_key", "dev_free", "host_free"])
-                c = r.randrange(2)
+                c = r.randrange(nctx)
                 if op == "switch":
                     with locks[c].exclusive():
                         cur[c] ^= 1
@@ -229,8 +239,11 @@ def main():
 
     ths = [threading.Thread(target=worker, args=(0, 1, ["cert3", "cert3", "cert8", "cert67", "cert129"])),
            threading.Thread(target=worker, args=(0, 2, ["host_batch", "dev_batch", "cert3"])),
-           threading.Thread(target=worker, args=(1, 3, ["cert3", "cert67", "cert8", "dev_batch"])),
+           threading.Thread(target=worker, args=(1, 3, ["cert3", "cert67", "cert8", "dev_batch"]
+                                                 + (["idle"] if nctx > 2 else []))),
            threading.Thread(target=control)]
+    ths += [threading.Thread(target=worker, args=(c, 10 + c, ["cert3", "cert3", "cert8", "cert67", "idle"]))
+            for c in range(2, nctx)]
     t0 = time.perf_counter()
     for t in ths:
         t.start()
@@ -246,9 +259,10 @@ def main():
     for t in ths:
         t.join(timeout=60)
     hung = [i for i, t in enumerate(ths) if t.is_alive()]
+    qc = [{k: int(v.qc_counters(0)[k]) for k in ("calls", "armed", "launches", "armings")} for v in ctxs]
     for v in ctxs:
         v.close()
-    out = {"seconds": time.perf_counter() - t0, "counts": counts, "wrong": len(wrong), "wrong_detail": wrong[:20],
+    out = {"seconds": time.perf_counter() - t0, "contexts": nctx, "qc_counters": qc, "counts": counts, "wrong": len(wrong), "wrong_detail": wrong[:20],
            "errors": errors[:10], "hung_threads": hung,
            "env": {k: v for k, v in os.environ.items() if k.startswith("PBFTV")}}
     print(json.dumps(out), flush=True)
