@@ -639,6 +639,7 @@ hipError_t qc_streams_ready(Device& d) {
       return hipSuccess;
     }
     ++r.hiq_pairs[d.id];
+    r.hiq_wanted.erase(d.id);  // (served; another waiter asks again at its next call)
   }
   for (hipStream_t& q : d.qstream) {
     int lo = 0, hi = 0;
