@@ -50,7 +50,7 @@ def fresh_calls(ver, n_keys, sigs, count, seed, register=True):
                                    K[c * sigs:(c + 1) * sigs], quorum=sigs) for c in range(count)]
 
 
-def timed_calls(calls, sigs, gap_s=0.0, ver=None, serve=None):
+def timed_calls(calls, sigs, gap_s=0.0, ver=None, serve=None, clk=None):
     ts = []
     for call in calls:
         if gap_s:
@@ -63,6 +63,8 @@ def timed_calls(calls, sigs, gap_s=0.0, ver=None, serve=None):
             st = ver.qc_stamps(0)
             if "gpu_serve_us" in st:
                 serve.append(st["gpu_serve_us"])
+            if clk is not None and "sclk_mhz" in st:  # the mean shader clock over that serve
+                clk.append(st["sclk_mhz"])
     return ts
 
 
@@ -176,8 +178,8 @@ def part_load(ver, quick):
     db = ver.alloc(0, n // 8 + 1)
     out = {}
     timed_calls(calls[:20], 3)
-    si3, si67 = [], []
-    out["idle_3sigs_gap2ms"] = pct(timed_calls(calls[20:320], 3, 0.002, ver, si3))
+    si3, si67, ci3, cv3 = [], [], [], []
+    out["idle_3sigs_gap2ms"] = pct(timed_calls(calls[20:320], 3, 0.002, ver, si3, ci3))
     timed_calls(calls67[:10], 67)
     out["idle_67sigs_gap2ms"] = pct(timed_calls(calls67[10:110], 67, 0.002, ver, si67))
     out["idle_gpu_serve_us_p50"] = {"3sigs": float(np.median(si3)) if si3 else None,
@@ -196,10 +198,16 @@ def part_load(ver, quick):
     time.sleep(0.05)
     t0 = time.perf_counter()
     sv3, sv67 = [], []
-    out["loaded_3sigs_gap2ms"] = pct(timed_calls(calls[320:620], 3, 0.002, ver, sv3))
+    out["loaded_3sigs_gap2ms"] = pct(timed_calls(calls[320:620], 3, 0.002, ver, sv3, cv3))
     out["loaded_67sigs_gap2ms"] = pct(timed_calls(calls67[110:220], 67, 0.002, ver, sv67))
     out["loaded_gpu_serve_us_p50"] = {"3sigs": float(np.median(sv3)) if sv3 else None,
                                       "67sigs": float(np.median(sv67)) if sv67 else None}
+    # serve time = cycles / clock: how much of the loaded penalty is the clock
+    if si3 and sv3 and ci3 and cv3:
+        ki, kl = float(np.median(ci3)), float(np.median(cv3))
+        out["sclk_mhz_p50_3sigs"] = {"idle": ki, "loaded": kl}
+        out["serve_kcycles_p50_3sigs"] = {"idle": float(np.median(si3)) * ki * 1e-3,
+                                          "loaded": float(np.median(sv3)) * kl * 1e-3}
     dt = time.perf_counter() - t0
     b0 = done[0]
     stop.set()
