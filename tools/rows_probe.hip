@@ -11,7 +11,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <vector>
+#include <unistd.h>
 
 using namespace pbftv;
 
@@ -42,7 +44,37 @@ __global__ void __launch_bounds__(64 * kRowWaves) rows_probe_k(const uint8_t* __
   if (threadIdx.x == 0) wave_store_verdict(ok, i, n, bitmap, nullptr);
 }
 
-int main() {
+// Background load for the stage stamps (argv[1]): "gather" -- random 64-B
+// loads over a 4-GB buffer at about the rate the comb's table gathers stream
+// through L2 and HBM (~1.2 TB/s); "valu" -- 64-bit MAD chains, no memory; "both"; "none".  Two waves per
+// SIMD on every CU (room is left for the probe's eight waves), until the host
+// raises *stop (or a 3-s budget).
+__global__ void __launch_bounds__(256) load_k(const uint4* __restrict__ buf, uint64_t nlines, int mode,
+                                              const uint32_t* stop, uint32_t* __restrict__ sink, uint64_t budget) {
+  const uint64_t t0 = wall_clock64();
+  uint64_t x = 0x9E3779B97F4A7C15ull * (blockIdx.x * 256 + threadIdx.x + 1), acc = x;
+  for (int it = 0;; ++it) {
+    if ((it & 15) == 0 &&
+        (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0 || wall_clock64() - t0 > budget))
+      break;
+    if (mode & 1) {  // one random 64-B line per thread per ~7 us: ~1.2 TB/s over the chip, the comb's gather rate
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      const uint4 v = buf[(x >> 20) % nlines];
+      acc ^= (uint64_t)v.x + v.y + v.z + v.w;
+      __builtin_amdgcn_s_sleep(127);
+      __builtin_amdgcn_s_sleep(127);
+    }
+    if (mode & 2) {
+#pragma unroll
+      for (int k = 0; k < 256; ++k) acc = ((uint64_t)(uint32_t)acc * ((uint32_t)(acc >> 29) | 1u) + acc) ^ (uint64_t)k;
+    }
+  }
+  if (acc == 0x123456789ull) sink[0] = (uint32_t)acc;
+}
+
+int main(int argc, char** argv) {
+  const char* lmode = argc > 1 ? argv[1] : "none";
+  const int mode = !strcmp(lmode, "gather") ? 1 : !strcmp(lmode, "valu") ? 2 : !strcmp(lmode, "both") ? 3 : 0;
   const uint32_t n = 64;
   // key = G (valid), random in-range r, s, e: the stages run in full whatever the verdict
   std::vector<uint8_t> h(32 * n), sg(64 * n), key(64);
@@ -97,12 +129,36 @@ int main() {
   const int stages[] = {1, 2, 3, 4, 5, 7, 8, 9, 10, 12, 13};
   const char* names[] = {"scalars", "handoff", "digits_entries", "level0_mmadd", "wave_pair_add", "l1_barrier",
                          "l1_add", "l2_barrier", "l2_add", "l3_barrier", "l3_check"};
-  printf("{\"geometry\": [%d, %d]", WG, WQ);
+  printf("{\"geometry\": [%d, %d], \"load\": \"%s\"", WG, WQ, lmode);
+  const uint64_t kLines = (4ull << 30) / 16;
+  uint4* lbuf = nullptr;
+  uint32_t* lstop = nullptr;
+  hipStream_t ls = nullptr;
+  if (mode) {
+    CHECK(hipMalloc(&lbuf, kLines * 16));
+    CHECK(hipMemset(lbuf, 0x5A, kLines * 16));
+    CHECK(hipHostMalloc(&lstop, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    CHECK(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
+    CHECK(hipDeviceSynchronize());
+  }
+  int ncu = 0;
+  CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   for (uint32_t nb : {1u, 3u, 64u}) {
+    if (mode) {  // the load runs for the whole rep loop, then stops
+      *(volatile uint32_t*)lstop = 0;
+      hipLaunchKernelGGL(load_k, dim3(2 * ncu), dim3(256), 0, ls, lbuf, kLines, mode, lstop, dsink,
+                         (uint64_t)rate_khz * 3000);
+      CHECK(hipGetLastError());
+      usleep(20000);
+    }
     for (int rep = 0; rep < 4; ++rep) {
       hipLaunchKernelGGL(rows_probe_k, dim3(nb), dim3(64 * RowsGeom<WG, WQ>::waves), 0, 0, dh, ds, dk, (uint64_t)nb, dvalid, 1u,
                          reinterpret_cast<const uint4*>(gt), reinterpret_cast<const uint4* const*>(dq), dbm);
-      CHECK(hipDeviceSynchronize());
+      CHECK(hipStreamSynchronize(0));  // (not the device: the load kernel runs on)
+    }
+    if (mode) {
+      *(volatile uint32_t*)lstop = 1;
+      CHECK(hipStreamSynchronize(ls));
     }
     std::vector<uint64_t> st(128 * 8 * kS);
     CHECK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_rows_probe), 8 * 128 * 8 * kS));
