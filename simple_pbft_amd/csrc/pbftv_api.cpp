@@ -618,7 +618,7 @@ int hiq_pair_cap() {
   static const int cap = [] {
     const char* e = getenv("GPU_MAX_HW_QUEUES");
     const int q = e && atoi(e) > 0 ? atoi(e) : 4;
-    return std::max(1, q / 2);
+    return q / 2;  // (one queue: no pair -- a successor would wait behind its predecessor)
   }();
   return cap;
 }

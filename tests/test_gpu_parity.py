@@ -798,7 +798,9 @@ def test_armed_stream_pairs_shared_out(oracle_lib, monkeypatch):
     import time
     from simple_pbft_amd import Verifier
     monkeypatch.setenv("PBFTV_QC_ARM_MS", "5000")
-    cap = max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) // 2)
+    cap = int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) // 2
+    if cap == 0:
+        pytest.skip("GPU_MAX_HW_QUEUES < 2: the library arms no server")
     keys, hashes, sigs, kidx = oracle_sign_pool(oracle_lib, n_keys=3, per_key=12, seed=83)
     sigs[::4, 45] ^= 0x20
     n_all = len(kidx)
